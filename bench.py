@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: CPIs/s through PC -> MTD -> 0-v -> 2-D CA-CFAR (BASELINE.json metric).
+
+Workload (config c3 of BASELINE.json): 128 pulses x 4096 range bins, complex fp32 echo,
+batch 1024 CPIs per GPU, `v2` preset (fun_MTD_produce's 3-segment pulse compression,
+kaiser-8 MTD with fftshift, 0-v /150) followed by main_cfar's /20 0-v and executeCFAR per
+PC segment (ref 5, guard 7, T 5, GO, range CFAR on).  A step is one pass of the chain
+over the batch, inputs resident in HBM.  Synthetic echoes (SURVEY.md §8d recipe, noise
+drawn on the GPU).
+
+Multi-GPU: one process per GPU (torchrun); each rank owns a contiguous shard of the CPI
+stream (weak scaling, no data-path collective: CPIs are independent); the only collectives
+are the timing barrier and the max-over-ranks of the elapsed time.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md for the roofline accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "radar-signal-process_amd"))
+
+METRIC = "CPIs/sec (4096 range × 128 pulse) through PC→MTD→CFAR; achieved HBM GB/s"
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--preset", default="v2", choices=["v2", "dmx"])
+    ap.add_argument("--P", type=int, default=128)
+    ap.add_argument("--R", type=int, default=4096)
+    ap.add_argument("--batch", type=int, default=1024, help="CPIs per GPU per step")
+    ap.add_argument("--no-cfar", action="store_true", help="PC + MTD only (config c2)")
+    ap.add_argument("--half", action="store_true", help="fp16 I/Q input (config c5 style)")
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
+    return ap.parse_args()
+
+
+def cpu_baseline(spec, cfar, seconds):
+    """fp64 C restatement (oracle/rsp_oracle.c, OpenMP over CPIs) on a bounded sample."""
+    if seconds <= 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import coracle
+    from rsp import synth
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = min(threads, 16)
+    pool_n = max(threads, 16)
+    echo = synth.echo_numpy(spec, pool_n, seed=1003).astype(np.complex128)
+    pre = coracle.preset(spec.name, spec.P, spec.R)
+    c = cfar.as_dict() if cfar is not None else None
+    if c is not None:
+        c["zero_v_div"] = cfar.zero_v_div
+    done, t0 = 0, time.perf_counter()
+    while True:
+        rdm = coracle.pc_mtd(echo, pre, nthreads=threads)
+        if c is not None:
+            coracle.cfar(rdm, c, cfar.segments, nthreads=threads)
+        done += pool_n
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "CPI/s", "cores": threads, "kind": "port",
+            "sample": "%d CPIs (%d x %d, %s preset%s) in %.1f s: a pool of %d distinct synthetic CPIs "
+                      "cycled; fp64 C restatement of the MATLAB chain (MATLAB itself is not available)"
+                      % (done, spec.P, spec.R, spec.name, " + CFAR" if c else "", el, pool_n)}
+
+
+def pmc_traffic(tag):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary, if one exists."""
+    p = os.path.join(ROOT, "profiles", "pmc_%s.json" % tag)
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from rsp import presets, synth
+    from rsp.engine import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    spec = presets.make(args.preset, args.P, args.R)
+    cfar = None if args.no_cfar else presets.default_cfar(spec)
+    eng = Engine(spec, device=local, chunk=args.chunk)
+    B, P, R = args.batch, spec.P, spec.R_out
+    # contiguous shard of the CPI stream per rank: seed = 1000 + config id 3 + first CPI index
+    echo = synth.echo_torch(spec, B, seed=1003 + rank * B, device=dev, half=args.half)
+    rdm = torch.empty((B, P, R), dtype=torch.float32, device=dev)
+    flag = torch.empty((B, P, R), dtype=torch.uint8, device=dev) if cfar else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.run_dev(echo, rdm=rdm, flag=flag, cfar=cfar, stream=stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # per-kernel device time: an identical pass of `steps` steps with HIP events around every
+    # launch (on the launch stream), right after the timed region
+    kernels = None
+    if not args.no_profile:
+        eng.profile(True)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        kernels = eng.profile_read()
+        eng.profile(False)
+
+    if rank == 0:
+        esz = 4 if args.half else 8
+        in_b, rdm_b, flag_b = P * spec.R * esz, P * R * 4, (P * R if cfar else 0)
+        cpi_bytes = in_b + rdm_b + flag_b              # SURVEY.md §8d algorithmic bytes per CPI
+        total_cpis = world * B * args.steps
+        value = total_cpis / elapsed
+        per_gpu_cpis_s = B * args.steps / (gpu_ms / 1e3)
+        achieved = per_gpu_cpis_s * cpi_bytes / 1e9
+        roof = {"bound": "hbm", "kernel": "chain (pc_kernel + mtd_kernel + cfar_r_kernel)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "alg_bytes_per_cpi": cpi_bytes, "cpis_per_step": B}
+        if kernels:
+            ks = {}
+            for name, (ms, n) in kernels.items():
+                avg_us = ms * 1e3 / n
+                ks[name] = {"avg_us": round(avg_us, 2), "launches": n, "total_ms": round(ms, 3)}
+            roof["kernels"] = ks
+            roof["kernel_sum_ms_per_step"] = round(sum(v[0] for v in kernels.values()) / args.steps, 3)
+        tag = "%s_P%d_R%d%s%s" % (args.preset, args.P, args.R, "" if cfar else "_nocfar", "_f16" if args.half else "")
+        pmc = pmc_traffic(tag)
+        if pmc:
+            roof["traffic"] = pmc.get("hbm_bytes_per_cpi")
+            roof["traffic_note"] = pmc.get("note")
+        cpu = None
+        if world == 1:
+            cpu = cpu_baseline(spec, cfar, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "CPI/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if not args.half else "f32 (fp16 I/Q storage)",
+            "data": "synthetic (SURVEY.md §8d echo: 3 targets + zero-Doppler clutter + CN(0,1) noise, GPU-drawn)",
+            "config": {"workload": "c3: %d pulses x %d range bins, %d CPIs per GPU per step, preset %s, "
+                                   "PC->MTD->0v%s" % (P, spec.R, B, args.preset,
+                                                      "->2D CA-CFAR (executeCFAR per PC segment)" if cfar else ""),
+                       "pulses": P, "range_bins": spec.R, "batch_per_gpu": B, "preset": args.preset,
+                       "input": "c32f16" if args.half else "c64",
+                       "parallelism": "frame-sharded x%d, no collective" % world},
+            "hbm_GBps_per_gpu": round(achieved, 1),
+            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+/*
+ * rsp.h -- C ABI of the MI355X range-Doppler engine (pulse compression -> MTD ->
+ * zero-velocity suppression -> 2-D CA-CFAR), the drop-in boundary for the hot path
+ * of XuZerui2023/Radar-Signal-Process.
+ *
+ * Plain C linkage, plain pointers and int64 sizes; no C++ or torch types cross it.
+ * Each entry point cites the MATLAB interface it replaces (paths relative to the
+ * reference root):
+ *
+ *   rsp_pc_mtd        MTD_Signal = fun_MTD_produce(echoData, params)
+ *                     (MTD/fun_MTD_produce.m:12; legacy 1-arg form
+ *                      MatlabProcess_xuzerui/fun_MTD_produce.m:3; callers
+ *                      MTD/main_produce_dataset_win_xzr_v2.m:136,
+ *                      MatlabProcess_xuzerui/main_produce_dataset_win_xzr.m:37-38)
+ *   rsp_cfar          [flag, flagV] = executeCFAR(rdm, refR, saveR, TR, mR,
+ *                                                 refV, saveV, TV, mV, M0, rFlag)
+ *                     (MatlabProcess_xuzerui/CFAR_WangCai/executeCFAR.m:1-2), and with
+ *                     nseg > 1 the segmented cfarFlag = fun_CFARflag(...)
+ *                     (CFAR_WangCai/main_cfar.m:142-161, a local function there),
+ *                     optionally preceded by main_cfar.m:88-91's fun_0v_pressing
+ *   rsp_pc_mtd_cfar   the fused chain fun_MTD_produce -> main_cfar's per-window CFAR
+ *                     (MTD/main_produce_dataset_win_xzr_v2.m:136 then
+ *                      CFAR_WangCai/main_cfar.m:88-93)
+ *
+ * Conventions
+ *   - Every call returns an int status (RSP_OK = 0); the message of the last failure
+ *     is rsp_last_error(ctx) (ctx == NULL: the last rsp_create failure).
+ *   - Host-buffer entry points (no _dev suffix) are synchronous; the caller owns the
+ *     host buffers, the context owns its device buffers (grow-only pool).
+ *   - _dev entry points take device pointers and enqueue on `stream` (a hipStream_t,
+ *     NULL = the null stream); they return before the work completes.
+ *   - One context per host thread and device.  MATLAB calls MEX on one thread.
+ *   - Device layouts are row-major C order: echo [batch][P][R] complex (interleaved
+ *     I/Q), RDM [batch][Nd][R_out] float32, flags [batch][Nd][R_out] uint8 0/1, where
+ *     Nd = P (Doppler bins) and R_out = params.R_out.
+ *   - Host-buffer entry points accept MATLAB column-major (RSP_COLMAJOR: element
+ *     (p, r) at r*P + p) or row-major data and convert on the device.
+ */
+#ifndef RSP_H
+#define RSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSP_ABI_VERSION 1
+#define RSP_MAX_SEG 4
+#define RSP_MAX_FIR_TAPS 64
+
+typedef struct rsp_ctx rsp_ctx;
+
+typedef enum {
+    RSP_OK = 0,
+    RSP_ERR_ARG = 1,          /* bad pointer / enum / size */
+    RSP_ERR_SHAPE = 2,        /* P, R, batch inconsistent with the context's params */
+    RSP_ERR_UNSUPPORTED = 3,  /* valid in MATLAB but not built here (e.g. odd FFT size) */
+    RSP_ERR_CFAR_WINDOW = 4,  /* a CFAR window does not fit: MATLAB raises an index error */
+    RSP_ERR_HIP = 5,          /* HIP runtime error (message has the HIP string) */
+    RSP_ERR_NOMEM = 6
+} rsp_status;
+
+typedef enum {
+    RSP_C64 = 0,        /* complex float32, interleaved re,im */
+    RSP_C128 = 1,       /* complex float64, interleaved (MATLAB R2018a mxGetComplexDoubles) */
+    RSP_C32F16 = 2      /* complex float16, interleaved (fp16 I/Q, fp32 compute) */
+} rsp_dtype;
+
+typedef enum {
+    RSP_ROWMAJOR = 0,   /* [P][R]: one pulse (PRT) per row, range contiguous */
+    RSP_COLMAJOR = 1    /* MATLAB P x R: [R][P], pulses contiguous */
+} rsp_layout;
+
+typedef enum {
+    RSP_SEG_FIR = 0,    /* y = scale * filter(taps, 1, x) then circshift(y, -fir_shift)
+                           (MTD/fun_lss_pulse_compression.m:38-51) */
+    RSP_SEG_MF = 1      /* y[n] = sum_k x[n+k] * conj(s[k]), x zero past in_len and
+                           periodic with period nfft (circular when in_len == nfft):
+                           MTD/fun_pulse_compression.m:10-39 (linear, nfft >= in_len +
+                           coef_len - 1) or DMX_SignalProcessing_main_xzr.m:348-352 */
+} rsp_seg_kind;
+
+typedef enum {
+    RSP_WIN_KAISER = 0,   /* kaiser(P, window_beta)  (MTD/fun_Process_MTD.m:17-18) */
+    RSP_WIN_HAMMING = 1,  /* hamming(P)  (DMX_SignalProcessing_main_xzr.m:211) */
+    RSP_WIN_RECT = 2
+} rsp_window;
+
+typedef struct {
+    int32_t kind;          /* rsp_seg_kind */
+    int32_t fir_shift;     /* FIR: out[n] = z[(n + fir_shift) mod out_len] */
+    int64_t in_start;      /* input columns [in_start, in_start + in_len) */
+    int64_t in_len;
+    int64_t out_start;     /* output columns [out_start, out_start + out_len) */
+    int64_t out_len;       /* FIR: out_len == in_len; MF: out_len <= nfft */
+    int64_t nfft;          /* MF: FFT length, 2^k or 3*2^k, 64 <= nfft <= 16384 */
+    double scale;          /* FIR: output scale (1/1.2 for the v2/legacy short pulse);
+                              MF: replica scale */
+    int64_t coef_len;      /* FIR: taps (<= RSP_MAX_FIR_TAPS); MF: replica length */
+    const double* coef_re; /* FIR taps / MF replica real part (copied at rsp_create) */
+    const double* coef_im; /* MF replica imaginary part (NULL = 0) */
+} rsp_pc_segment;
+
+typedef struct {
+    int64_t P;             /* pulses per CPI: 2^k or 3*2^k, 16 <= P <= 1536 */
+    int64_t R;             /* input range bins per pulse */
+    int64_t R_out;         /* output range bins (PC output = RDM columns) */
+    int32_t nseg;          /* pulse-compression segments (<= RSP_MAX_SEG) */
+    int32_t window;        /* rsp_window for the slow-time FFT */
+    double window_beta;    /* kaiser beta (8 in fun_Process_MTD) */
+    int32_t fftshift;      /* 1: fftshift the Doppler axis (fun_Process_MTD.m:31) */
+    int32_t zero_v_div;    /* fun_0v_pressing divisor (150 in MTD/fun_0v_pressing.m:22);
+                              0 = no suppression */
+    rsp_pc_segment seg[RSP_MAX_SEG];
+} rsp_params;
+
+typedef struct {
+    int32_t refR, saveR, methodR;   /* range CFAR: reference, guard cells, 0 GO / 1 SO */
+    double TR;                      /* range CFAR threshold factor */
+    int32_t refV, saveV, methodV;   /* Doppler CFAR */
+    double TV;
+    int32_t M0;                     /* MTD_0_num: strips rows 1..M0+1 and V-M0+1..V */
+    int32_t rFlag;                  /* 1: range CFAR on the Doppler hits; 0: flag = flagV */
+    int32_t zero_v_div;             /* fun_0v_pressing before CFAR (20 in
+                                       CFAR_WangCai/fun_0v_pressing.m:5); 0 = none */
+    int32_t nseg;                   /* column segments; 0 = one segment, all columns */
+    int64_t seg_lo[RSP_MAX_SEG];    /* 0-based [seg_lo, seg_hi); columns outside every
+                                       segment get flag 0 (main_cfar.m:156-159) */
+    int64_t seg_hi[RSP_MAX_SEG];
+} rsp_cfar_params;
+
+/* Library version string, e.g. "rsp-mi355x 0.1.0 (gfx950)". */
+const char* rsp_version(void);
+
+/* Create a context bound to HIP device `device` for one parameter set.  Builds the
+ * matched-filter spectra (fp64 on the host, stored fp32), twiddle tables and window. */
+int rsp_create(rsp_ctx** out, int device, const rsp_params* params);
+int rsp_destroy(rsp_ctx* ctx);
+const char* rsp_last_error(const rsp_ctx* ctx);
+
+/* CPIs processed per internal chunk (PC scratch = chunk * P * R_out * 8 bytes, sized to
+ * stay in the 256 MiB Infinity Cache).  0 restores the default. */
+int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
+
+/* ---- host-buffer entry points (MEX / fun_MTD_produce drop-in), synchronous ---------- */
+int rsp_pc_mtd(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,
+               int64_t P, int64_t R, int64_t batch, float* rdm_out, int32_t rdm_layout);
+
+int rsp_cfar(rsp_ctx* ctx, const float* rdm, int32_t rdm_layout, int64_t V, int64_t R,
+             int64_t batch, const rsp_cfar_params* cfar, uint8_t* flag_out,
+             uint8_t* flagV_out /* nullable */);
+
+int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,
+                    int64_t P, int64_t R, int64_t batch, const rsp_cfar_params* cfar,
+                    float* rdm_out /* nullable */, int32_t out_layout, uint8_t* flag_out,
+                    uint8_t* flagV_out /* nullable */);
+
+/* ---- device-pointer entry points, asynchronous on `stream` -------------------------- */
+/* d_echo: [batch][P][R] rsp_dtype RSP_C64 or RSP_C32F16.  cfar == NULL: PC + MTD only.
+ * d_rdm may be NULL only when cfar != NULL (then an internal buffer is used). */
+int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,
+                        const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag,
+                        uint8_t* d_flagV, void* stream);
+
+int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t batch,
+                 const rsp_cfar_params* cfar, uint8_t* d_flag, uint8_t* d_flagV,
+                 void* stream);
+
+/* Pulse compression alone (fun_lss_pulse_compression), for tests and staged use:
+ * d_pc = [batch][P][R_out] complex float32. */
+int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, void* d_pc,
+               void* stream);
+
+/* ---- diagnostics ---------------------------------------------------------------------- */
+/* Per-kernel device time accumulated from HIP events recorded on the launch stream around
+ * every kernel while profiling is enabled (enable = 1 also resets the counters).
+ * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V. */
+#define RSP_NKERNELS 4
+enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3 };
+int rsp_profile(rsp_ctx* ctx, int32_t enable);
+/* Waits for the recorded events; ms[k] = summed device time, launches[k] = launch count. */
+int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSP_H */

@@ -1,0 +1,705 @@
+// rsp_capi.cpp -- the C ABI (include/rsp.h): context, parameter validation, fp64 host
+// precomputation (matched-filter spectra, twiddle tables, windows), device buffer pools
+// and the chunked PC -> MTD(+Doppler CFAR) -> range CFAR pipeline.
+//
+// Chunking: the pulse-compression output of `chunk` CPIs is written to a scratch buffer
+// that is read back by the MTD kernel right after; chunk * P * R_out * 8 bytes is sized
+// (default 32 MiB) to stay in the 256 MiB Infinity Cache, so the corner turn between
+// the fast-time (PC) and slow-time (MTD) passes is served on-die instead of from HBM.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/rsp.h"
+#include "rsp_internal.h"
+
+using cd = std::complex<double>;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+struct rsp_ctx {
+    int device = 0;
+    rsp_params p{};
+    std::string err;
+    hipStream_t stream = nullptr;
+    rsp::PcArgs pc{};
+    rsp::MtdArgs mtd{};
+    size_t pc_lds = 0;
+    int64_t chunk = 0;  // 0 = default
+    std::vector<void*> owned;           // constant tables (freed at destroy)
+    std::map<int, float2*> tw;          // twiddle tables by length
+    DevBuf scratch_pc, tmp_flagV, tmp_rdm;
+    DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
+    // diagnostics (rsp_profile): HIP event pairs around each kernel launch
+    struct Ev {
+        int k;
+        hipEvent_t a, b;
+    };
+    bool prof = false;
+    std::vector<Ev> evs;
+    size_t nev = 0;
+    double prof_ms[RSP_NKERNELS] = {};
+    int64_t prof_n[RSP_NKERNELS] = {};
+};
+
+static thread_local std::string g_err;
+
+static int fail(rsp_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail((ctx), RSP_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                        __FILE__, __LINE__);                                                 \
+    } while (0)
+
+// ------------------------------------------------------------------ host numerics (fp64)
+static double mround(double x) { return x >= 0 ? std::floor(x + 0.5) : -std::floor(-x + 0.5); }
+
+static double bessel_i0(double x) {
+    double sum = 1.0, term = 1.0, q = x * x / 4.0;
+    for (int k = 1; k < 500; ++k) {
+        term *= q / ((double)k * k);
+        sum += term;
+        if (term < 1e-18 * sum) break;
+    }
+    return sum;
+}
+
+static std::vector<double> make_window(int kind, double beta, int64_t n) {
+    std::vector<double> w((size_t)n, 1.0);
+    if (n == 1) return w;
+    for (int64_t k = 0; k < n; ++k) {
+        if (kind == RSP_WIN_KAISER) {
+            double r = ((double)k - (n - 1) / 2.0) / ((n - 1) / 2.0);
+            double a = 1.0 - r * r;
+            w[k] = bessel_i0(beta * std::sqrt(a > 0 ? a : 0.0)) / bessel_i0(beta);
+        } else if (kind == RSP_WIN_HAMMING) {
+            w[k] = 0.54 - 0.46 * std::cos(2.0 * M_PI * (double)k / (double)(n - 1));
+        }
+    }
+    return w;
+}
+
+// in-place radix-2 forward FFT, n a power of two
+static void fft_pow2(std::vector<cd>& a) {
+    const size_t n = a.size();
+    for (size_t i = 1, j = 0; i < n; ++i) {
+        size_t bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) std::swap(a[i], a[j]);
+    }
+    for (size_t len = 2; len <= n; len <<= 1) {
+        for (size_t i = 0; i < n; i += len) {
+            for (size_t k = 0; k < len / 2; ++k) {
+                const double ang = -2.0 * M_PI * (double)k / (double)len;
+                const cd w(std::cos(ang), std::sin(ang));
+                const cd u = a[i + k], v = a[i + k + len / 2] * w;
+                a[i + k] = u + v;
+                a[i + k + len / 2] = u - v;
+            }
+        }
+    }
+}
+
+template <typename T>
+static int upload(rsp_ctx* ctx, const std::vector<T>& h, T** out) {
+    void* d = nullptr;
+    HIP_TRY(ctx, hipMalloc(&d, h.size() * sizeof(T)));
+    ctx->owned.push_back(d);
+    HIP_TRY(ctx, hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = (T*)d;
+    return RSP_OK;
+}
+
+static int twiddles(rsp_ctx* ctx, int n, const float2** out) {
+    auto it = ctx->tw.find(n);
+    if (it != ctx->tw.end()) {
+        *out = it->second;
+        return RSP_OK;
+    }
+    std::vector<float2> h((size_t)n);
+    for (int e = 0; e < n; ++e) {
+        const double ang = -2.0 * M_PI * (double)e / (double)n;
+        h[e] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+    }
+    float2* d = nullptr;
+    int rc = upload(ctx, h, &d);
+    if (rc) return rc;
+    ctx->tw[n] = d;
+    *out = d;
+    return RSP_OK;
+}
+
+static int ensure(rsp_ctx* ctx, DevBuf& b, size_t bytes) {
+    if (b.n >= bytes && b.p) return RSP_OK;
+    if (b.p) {
+        HIP_TRY(ctx, hipFree(b.p));
+        b.p = nullptr;
+        b.n = 0;
+    }
+    if (bytes == 0) return RSP_OK;
+    HIP_TRY(ctx, hipMalloc(&b.p, bytes));
+    b.n = bytes;
+    return RSP_OK;
+}
+
+static void zero_v_band(int64_t rows, int div, int* lo, int* hi) {
+    if (div <= 0) {
+        *lo = 0;
+        *hi = 0;
+        return;
+    }
+    const int64_t zv = (int64_t)mround(rows / 2.0);
+    const int64_t k = (int64_t)mround((double)rows / (double)div);
+    int64_t a = zv - k - 1, b = zv + k;
+    if (a < 0) a = 0;
+    if (b > rows) b = rows;
+    *lo = (int)a;
+    *hi = (int)(b > a ? b : a);
+}
+
+// ------------------------------------------------------------------ public API
+const char* rsp_version(void) { return "rsp-mi355x 0.1.0 (gfx950, abi 1)"; }
+
+const char* rsp_last_error(const rsp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int rsp_destroy(rsp_ctx* ctx) {
+    if (!ctx) return RSP_OK;
+    hipSetDevice(ctx->device);
+    for (void* p : ctx->owned) hipFree(p);
+    DevBuf* bufs[] = {&ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->st_in, &ctx->st_canon,
+                      &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t};
+    for (DevBuf* b : bufs)
+        if (b->p) hipFree(b->p);
+    for (auto& e : ctx->evs) {
+        hipEventDestroy(e.a);
+        hipEventDestroy(e.b);
+    }
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return RSP_OK;
+}
+
+int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
+    if (!out || !prm) return fail(nullptr, RSP_ERR_ARG, "rsp_create: null argument");
+    *out = nullptr;
+    const rsp_params& p = *prm;
+    if (p.P < 2 || p.R < 1 || p.R_out < 1 || p.R > (1 << 24) || p.R_out > (1 << 24))
+        return fail(nullptr, RSP_ERR_SHAPE, "rsp_create: bad P=%lld R=%lld R_out=%lld",
+                    (long long)p.P, (long long)p.R, (long long)p.R_out);
+    if (!rsp::mtd_size_supported((int)p.P))
+        return fail(nullptr, RSP_ERR_UNSUPPORTED,
+                    "rsp_create: P=%lld pulses not built (supported: 2^k or 3*2^k, 16..1536)",
+                    (long long)p.P);
+    if (p.nseg < 0 || p.nseg > RSP_MAX_SEG)
+        return fail(nullptr, RSP_ERR_ARG, "rsp_create: nseg=%d out of range", p.nseg);
+    if (p.window < RSP_WIN_KAISER || p.window > RSP_WIN_RECT)
+        return fail(nullptr, RSP_ERR_ARG, "rsp_create: bad window %d", p.window);
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, RSP_ERR_HIP, "rsp_create: no HIP device available");
+    if (device < 0 || device >= ndev)
+        return fail(nullptr, RSP_ERR_ARG, "rsp_create: device %d out of range (%d devices)", device, ndev);
+
+    rsp_ctx* ctx = new rsp_ctx();
+    ctx->device = device;
+    ctx->p = p;
+    for (int s = 0; s < RSP_MAX_SEG; ++s) ctx->p.seg[s].coef_re = ctx->p.seg[s].coef_im = nullptr;
+    auto bail = [&](int rc) {
+        g_err = ctx->err;
+        rsp_destroy(ctx);
+        return rc;
+    };
+    if (hipSetDevice(device) != hipSuccess) return bail(fail(ctx, RSP_ERR_HIP, "hipSetDevice(%d) failed", device));
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(ctx, RSP_ERR_HIP, "hipStreamCreate failed"));
+
+    // ---- pulse-compression segments
+    rsp::PcArgs& pc = ctx->pc;
+    pc.P = (int)p.P;
+    pc.R = (int)p.R;
+    pc.R_out = (int)p.R_out;
+    pc.nseg = p.nseg;
+    std::vector<char> covered((size_t)p.R_out, 0);
+    int max_nfft = 64;
+    for (int s = 0; s < p.nseg; ++s) {
+        const rsp_pc_segment& g = p.seg[s];
+        rsp::SegDev& d = pc.seg[s];
+        std::memset(&d, 0, sizeof(d));
+        if (g.in_start < 0 || g.in_len < 1 || g.in_start + g.in_len > p.R)
+            return bail(fail(ctx, RSP_ERR_ARG, "segment %d: input [%lld,+%lld) outside R=%lld", s,
+                             (long long)g.in_start, (long long)g.in_len, (long long)p.R));
+        if (g.out_start < 0 || g.out_len < 1 || g.out_start + g.out_len > p.R_out)
+            return bail(fail(ctx, RSP_ERR_ARG, "segment %d: output [%lld,+%lld) outside R_out=%lld", s,
+                             (long long)g.out_start, (long long)g.out_len, (long long)p.R_out));
+        for (int64_t c = g.out_start; c < g.out_start + g.out_len; ++c) {
+            if (covered[c]) return bail(fail(ctx, RSP_ERR_ARG, "segment %d overlaps another segment's output", s));
+            covered[c] = 1;
+        }
+        if (!g.coef_re || g.coef_len < 1)
+            return bail(fail(ctx, RSP_ERR_ARG, "segment %d: missing coefficients", s));
+        d.kind = g.kind;
+        d.in_start = (int)g.in_start;
+        d.in_len = (int)g.in_len;
+        d.out_start = (int)g.out_start;
+        d.out_len = (int)g.out_len;
+        d.scale = (float)g.scale;
+        if (g.kind == RSP_SEG_FIR) {
+            if (g.coef_len > RSP_MAX_FIR_TAPS)
+                return bail(fail(ctx, RSP_ERR_UNSUPPORTED, "segment %d: %lld FIR taps > %d", s,
+                                 (long long)g.coef_len, RSP_MAX_FIR_TAPS));
+            if (g.out_len != g.in_len)
+                return bail(fail(ctx, RSP_ERR_ARG, "segment %d: FIR needs out_len == in_len", s));
+            d.ntaps = (int)g.coef_len;
+            for (int k = 0; k < d.ntaps; ++k) d.taps[k] = (float)g.coef_re[k];
+            int64_t sh = g.fir_shift % g.out_len;
+            if (sh < 0) sh += g.out_len;
+            d.fir_shift = (int)sh;
+        } else if (g.kind == RSP_SEG_MF) {
+            if (!rsp::pc_nfft_supported((int)g.nfft))
+                return bail(fail(ctx, RSP_ERR_UNSUPPORTED, "segment %d: nfft=%lld not built (2^k, 64..16384)", s,
+                                 (long long)g.nfft));
+            if (g.in_len > g.nfft || g.out_len > g.nfft)
+                return bail(fail(ctx, RSP_ERR_ARG, "segment %d: in_len/out_len exceed nfft", s));
+            d.nfft = (int)g.nfft;
+            if (d.nfft > max_nfft) max_nfft = d.nfft;
+            // H = conj(FFT_nfft(scale * replica)) / nfft, in fp64 (fft(x, n) truncates)
+            std::vector<cd> a((size_t)g.nfft, cd(0, 0));
+            const int64_t L = g.coef_len < g.nfft ? g.coef_len : g.nfft;
+            for (int64_t k = 0; k < L; ++k)
+                a[k] = g.scale * cd(g.coef_re[k], g.coef_im ? g.coef_im[k] : 0.0);
+            fft_pow2(a);
+            std::vector<float2> h((size_t)g.nfft);
+            for (int64_t k = 0; k < g.nfft; ++k) {
+                const cd v = std::conj(a[k]) / (double)g.nfft;
+                h[k] = make_float2((float)v.real(), (float)v.imag());
+            }
+            float2* dh = nullptr;
+            int rc = upload(ctx, h, &dh);
+            if (rc) return bail(rc);
+            d.H = dh;
+            rc = twiddles(ctx, d.nfft, &d.tw);
+            if (rc) return bail(rc);
+        } else {
+            return bail(fail(ctx, RSP_ERR_ARG, "segment %d: bad kind %d", s, g.kind));
+        }
+    }
+    // output columns no segment writes stay 0 (s_PC_0 = zeros, fun_lss_pulse_compression.m:27)
+    pc.nzero = 0;
+    for (int64_t c = 0; c < p.R_out;) {
+        if (covered[c]) { ++c; continue; }
+        int64_t e = c;
+        while (e < p.R_out && !covered[e]) ++e;
+        if (pc.nzero >= RSP_MAX_SEG + 1)
+            return bail(fail(ctx, RSP_ERR_UNSUPPORTED, "too many uncovered output column ranges"));
+        pc.zero_lo[pc.nzero] = (int)c;
+        pc.zero_hi[pc.nzero] = (int)e;
+        ++pc.nzero;
+        c = e;
+    }
+    ctx->pc_lds = rsp::pc_lds_bytes(max_nfft);
+
+    // ---- MTD
+    rsp::MtdArgs& m = ctx->mtd;
+    m.P = (int)p.P;
+    m.R_out = (int)p.R_out;
+    m.shift = p.fftshift ? (int)(p.P / 2) : 0;
+    zero_v_band(p.P, p.zero_v_div, &m.z_lo, &m.z_hi);
+    std::vector<double> w = make_window(p.window, p.window_beta, p.P);
+    std::vector<float> wf(w.begin(), w.end());
+    float* dw = nullptr;
+    int rc = upload(ctx, wf, &dw);
+    if (rc) return bail(rc);
+    m.win = dw;
+    rc = twiddles(ctx, (int)p.P, &m.tw);
+    if (rc) return bail(rc);
+    *out = ctx;
+    return RSP_OK;
+}
+
+int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_chunk: null ctx");
+    if (cpis < 0) return fail(ctx, RSP_ERR_ARG, "rsp_set_chunk: negative chunk");
+    ctx->chunk = cpis;
+    return RSP_OK;
+}
+
+
+static int64_t chunk_of(const rsp_ctx* ctx, int64_t batch) {
+    int64_t c = ctx->chunk;
+    if (c <= 0) {
+        const int64_t per = ctx->p.P * ctx->p.R_out * 8;
+        c = (32ll << 20) / (per > 0 ? per : 1);
+        if (c < 1) c = 1;
+    }
+    if (c > batch) c = batch;
+    if (c > 65535) c = 65535;
+    return c;
+}
+
+// CFAR argument blocks from the public struct; validates like MATLAB would fail.
+static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_t R,
+                      rsp::CfarVArgs* cv, rsp::CfarRArgs* cr) {
+    if (cf->refV < 1 || cf->saveV < 0 || cf->refR < 1 || cf->saveR < 0)
+        return fail(ctx, RSP_ERR_ARG, "CFAR: reference cells must be >= 1 and guard cells >= 0");
+    if (cf->M0 < 0 || 2 * (int64_t)cf->M0 + 1 > V)
+        return fail(ctx, RSP_ERR_ARG, "CFAR: M0=%d leaves no rows of %lld", cf->M0, (long long)V);
+    if (cf->nseg < 0 || cf->nseg > RSP_MAX_SEG) return fail(ctx, RSP_ERR_ARG, "CFAR: bad nseg %d", cf->nseg);
+    const int lo = cf->M0 + 1, hi = (int)V - cf->M0;
+    if (hi - lo < 2 * (cf->saveV + cf->refV))
+        return fail(ctx, RSP_ERR_CFAR_WINDOW,
+                    "CFAR: %d Doppler cells after stripping M0 rows < 2*(guard+ref)=%d "
+                    "(Function_CFAR1D_sub would index out of range)",
+                    hi - lo, 2 * (cf->saveV + cf->refV));
+    int nseg = cf->nseg;
+    int64_t slo[RSP_MAX_SEG], shi[RSP_MAX_SEG];
+    if (nseg == 0) {
+        nseg = 1;
+        slo[0] = 0;
+        shi[0] = R;
+    } else {
+        for (int s = 0; s < nseg; ++s) {
+            slo[s] = cf->seg_lo[s];
+            shi[s] = cf->seg_hi[s];
+            if (slo[s] < 0 || shi[s] > R || shi[s] <= slo[s])
+                return fail(ctx, RSP_ERR_ARG, "CFAR: segment %d [%lld,%lld) outside [0,%lld)", s,
+                            (long long)slo[s], (long long)shi[s], (long long)R);
+            for (int q = 0; q < s; ++q)
+                if (slo[s] < shi[q] && slo[q] < shi[s]) return fail(ctx, RSP_ERR_ARG, "CFAR: segments overlap");
+        }
+    }
+    if (cf->rFlag)
+        for (int s = 0; s < nseg; ++s)
+            if (shi[s] - slo[s] < 2 * (cf->saveR + cf->refR))
+                return fail(ctx, RSP_ERR_CFAR_WINDOW,
+                            "CFAR: range segment %d has %lld cells < 2*(guard+ref)=%d", s,
+                            (long long)(shi[s] - slo[s]), 2 * (cf->saveR + cf->refR));
+    int cz_lo, cz_hi;
+    zero_v_band(V, cf->zero_v_div, &cz_lo, &cz_hi);
+    std::memset(cv, 0, sizeof(*cv));
+    cv->enabled = 1;
+    cv->lo = lo;
+    cv->hi = hi;
+    cv->ref = cf->refV;
+    cv->save = cf->saveV;
+    cv->method = cf->methodV;
+    cv->T = (float)cf->TV;
+    cv->cz_lo = cz_lo;
+    cv->cz_hi = cz_hi;
+    cv->nseg = nseg;
+    std::memset(cr, 0, sizeof(*cr));
+    cr->V = (int)V;
+    cr->R = (int)R;
+    cr->lo = lo;
+    cr->hi = hi;
+    cr->rflag = cf->rFlag ? 1 : 0;
+    cr->ref = cf->refR;
+    cr->save = cf->saveR;
+    cr->method = cf->methodR;
+    cr->T = (float)cf->TR;
+    cr->cz_lo = cz_lo;
+    cr->cz_hi = cz_hi;
+    cr->nseg = nseg;
+    for (int s = 0; s < nseg; ++s) {
+        cv->seg_lo[s] = cr->seg_lo[s] = (int)slo[s];
+        cv->seg_hi[s] = cr->seg_hi[s] = (int)shi[s];
+    }
+    return RSP_OK;
+}
+
+static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess; }
+
+// Run one kernel launch, bracketed by HIP events on `s` when profiling is on.
+template <typename F>
+static hipError_t timed(rsp_ctx* ctx, int k, hipStream_t s, F&& launch) {
+    if (!ctx->prof) return launch();
+    if (ctx->nev == ctx->evs.size()) {
+        rsp_ctx::Ev e{k, nullptr, nullptr};
+        hipError_t r = hipEventCreate(&e.a);
+        if (r == hipSuccess) r = hipEventCreate(&e.b);
+        if (r != hipSuccess) return r;
+        ctx->evs.push_back(e);
+    }
+    rsp_ctx::Ev& e = ctx->evs[ctx->nev++];
+    e.k = k;
+    hipError_t r = hipEventRecord(e.a, s);
+    if (r != hipSuccess) return r;
+    r = launch();
+    if (r != hipSuccess) return r;
+    return hipEventRecord(e.b, s);
+}
+
+int rsp_profile(rsp_ctx* ctx, int32_t enable) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_profile: null ctx");
+    ctx->prof = enable != 0;
+    ctx->nev = 0;
+    for (int k = 0; k < RSP_NKERNELS; ++k) {
+        ctx->prof_ms[k] = 0;
+        ctx->prof_n[k] = 0;
+    }
+    return RSP_OK;
+}
+
+int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches) {
+    if (!ctx || !ms || !launches) return fail(ctx, RSP_ERR_ARG, "rsp_profile_read: null argument");
+    for (size_t i = 0; i < ctx->nev; ++i) {
+        rsp_ctx::Ev& e = ctx->evs[i];
+        HIP_TRY(ctx, hipEventSynchronize(e.b));
+        float t = 0.f;
+        HIP_TRY(ctx, hipEventElapsedTime(&t, e.a, e.b));
+        ctx->prof_ms[e.k] += t;
+        ctx->prof_n[e.k] += 1;
+    }
+    ctx->nev = 0;
+    for (int k = 0; k < RSP_NKERNELS; ++k) {
+        ms[k] = ctx->prof_ms[k];
+        launches[k] = ctx->prof_n[k];
+    }
+    return RSP_OK;
+}
+
+int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, void* d_pc, void* stream) {
+    if (!ctx || !d_echo || !d_pc || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: bad argument");
+    if (dtype != RSP_C64 && dtype != RSP_C32F16) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: dtype %d", dtype);
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    HIP_TRY(ctx, rsp::launch_pc(d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, ctx->pc, ctx->pc_lds,
+                                (hipStream_t)stream));
+    return RSP_OK;
+}
+
+int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,
+                        const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                        void* stream) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: null ctx");
+    if (!d_echo || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: bad echo/batch");
+    if (dtype != RSP_C64 && dtype != RSP_C32F16)
+        return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: device dtype must be RSP_C64 or RSP_C32F16");
+    if (cfar && !d_flag) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: CFAR requested without d_flag");
+    if (!cfar && !d_rdm) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: no output requested");
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out;
+    const size_t esz = dtype == RSP_C64 ? 8 : 4;
+    rsp::MtdArgs m = ctx->mtd;
+    rsp::CfarRArgs cr{};
+    if (cfar) {
+        int rc = build_cfar(ctx, cfar, P, Ro, &m.cv, &cr);
+        if (rc) return rc;
+    } else {
+        m.cv.enabled = 0;
+    }
+    const int64_t chunk = chunk_of(ctx, batch);
+    int rc = ensure(ctx, ctx->scratch_pc, (size_t)chunk * P * Ro * sizeof(float2));
+    if (rc) return rc;
+    if (cfar && !d_flagV) {
+        rc = ensure(ctx, ctx->tmp_flagV, (size_t)chunk * P * Ro);
+        if (rc) return rc;
+    }
+    if (!d_rdm) {
+        rc = ensure(ctx, ctx->tmp_rdm, (size_t)chunk * P * Ro * sizeof(float));
+        if (rc) return rc;
+    }
+    for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+        const int64_t n = batch - c0 < chunk ? batch - c0 : chunk;
+        const char* ein = (const char*)d_echo + (size_t)c0 * P * R * esz;
+        float* rdm = d_rdm ? d_rdm + (size_t)c0 * P * Ro : (float*)ctx->tmp_rdm.p;
+        uint8_t* fv = nullptr;
+        if (cfar) fv = d_flagV ? d_flagV + (size_t)c0 * P * Ro : (uint8_t*)ctx->tmp_flagV.p;
+        float2* pcs = (float2*)ctx->scratch_pc.p;
+        HIP_TRY(ctx, timed(ctx, RSP_K_PC, s, [&] { return rsp::launch_pc(ein, dtype, pcs, n * P, ctx->pc, ctx->pc_lds, s); }));
+        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, s, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, s); }));
+        if (cfar) {
+            uint8_t* fl = d_flag + (size_t)c0 * P * Ro;
+            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, s, [&] { return rsp::launch_cfar_r(rdm, fv, fl, (int)n, cr, s); }));
+        }
+    }
+    return RSP_OK;
+}
+
+int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t batch,
+                 const rsp_cfar_params* cfar, uint8_t* d_flag, uint8_t* d_flagV, void* stream) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_cfar_dev: null ctx");
+    if (!d_rdm || !cfar || !d_flag || V < 1 || R < 1 || batch < 0)
+        return fail(ctx, RSP_ERR_ARG, "rsp_cfar_dev: bad argument");
+    if ((V + 1) * 4 > 64 * 1024 || R * 6 > 150 * 1024)
+        return fail(ctx, RSP_ERR_UNSUPPORTED, "rsp_cfar_dev: V=%lld or R=%lld too large", (long long)V, (long long)R);
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    rsp::CfarVArgs cv;
+    rsp::CfarRArgs cr;
+    int rc = build_cfar(ctx, cfar, V, R, &cv, &cr);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t chunk = 65535;
+    if (!d_flagV) {
+        rc = ensure(ctx, ctx->tmp_flagV, (size_t)(batch < chunk ? batch : chunk) * V * R);
+        if (rc) return rc;
+    }
+    for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+        const int64_t n = batch - c0 < chunk ? batch - c0 : chunk;
+        const float* rdm = d_rdm + (size_t)c0 * V * R;
+        uint8_t* fv = d_flagV ? d_flagV + (size_t)c0 * V * R : (uint8_t*)ctx->tmp_flagV.p;
+        uint8_t* fl = d_flag + (size_t)c0 * V * R;
+        HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_V, s, [&] { return rsp::launch_cfar_v(rdm, fv, (int)n, (int)V, (int)R, cv, s); }));
+        HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, s, [&] { return rsp::launch_cfar_r(rdm, fv, fl, (int)n, cr, s); }));
+    }
+    return RSP_OK;
+}
+
+// ------------------------------------------------------------------ host-buffer entry points
+static size_t dtype_size(int32_t dtype) {
+    switch (dtype) {
+        case RSP_C64: return 8;
+        case RSP_C128: return 16;
+        case RSP_C32F16: return 4;
+        default: return 0;
+    }
+}
+
+// H2D + conversion into the canonical device layout; returns the device echo pointer.
+static int stage_echo(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t batch,
+                      const void** d_echo, int32_t* d_dtype) {
+    const int64_t P = ctx->p.P, R = ctx->p.R;
+    const size_t esz = dtype_size(dtype);
+    const size_t bytes = (size_t)batch * P * R * esz;
+    int rc = ensure(ctx, ctx->st_in, bytes);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->st_in.p, echo, bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (layout == RSP_ROWMAJOR && (dtype == RSP_C64 || dtype == RSP_C32F16)) {
+        *d_echo = ctx->st_in.p;
+        *d_dtype = dtype;
+        return RSP_OK;
+    }
+    rc = ensure(ctx, ctx->st_canon, (size_t)batch * P * R * sizeof(float2));
+    if (rc) return rc;
+    HIP_TRY(ctx, rsp::launch_ingest(ctx->st_in.p, dtype, layout, (float2*)ctx->st_canon.p, batch, (int)P,
+                                    (int)R, ctx->stream));
+    *d_echo = ctx->st_canon.p;
+    *d_dtype = RSP_C64;
+    return RSP_OK;
+}
+
+template <typename T>
+static int fetch(rsp_ctx* ctx, const T* d, T* h, int64_t batch, int64_t A, int64_t B, int32_t layout) {
+    const size_t n = (size_t)batch * A * B;
+    if (layout == RSP_COLMAJOR) {
+        int rc = ensure(ctx, ctx->st_t, n * sizeof(T));
+        if (rc) return rc;
+        hipError_t e;
+        if (sizeof(T) == 4)
+            e = rsp::launch_transpose_f32((const float*)d, (float*)ctx->st_t.p, batch, (int)A, (int)B, ctx->stream);
+        else
+            e = rsp::launch_transpose_u8((const uint8_t*)d, (uint8_t*)ctx->st_t.p, batch, (int)A, (int)B, ctx->stream);
+        HIP_TRY(ctx, e);
+        d = (const T*)ctx->st_t.p;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return RSP_OK;
+}
+
+static int check_host_call(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P,
+                           int64_t R, int64_t batch) {
+    if (!echo || batch < 0) return fail(ctx, RSP_ERR_ARG, "null echo or negative batch");
+    if (!dtype_size(dtype)) return fail(ctx, RSP_ERR_ARG, "bad dtype %d", dtype);
+    if (layout != RSP_ROWMAJOR && layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad layout %d", layout);
+    if (P != ctx->p.P || R != ctx->p.R)
+        return fail(ctx, RSP_ERR_SHAPE, "echo is %lld x %lld but the context was created for %lld x %lld",
+                    (long long)P, (long long)R, (long long)ctx->p.P, (long long)ctx->p.R);
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    return RSP_OK;
+}
+
+int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                    int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
+                    uint8_t* flag_out, uint8_t* flagV_out) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "null ctx");
+    int rc = check_host_call(ctx, echo, dtype, layout, P, R, batch);
+    if (rc) return rc;
+    if (out_layout != RSP_ROWMAJOR && out_layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad out_layout");
+    if (cfar && !flag_out) return fail(ctx, RSP_ERR_ARG, "CFAR requested without flag_out");
+    if (!cfar && !rdm_out) return fail(ctx, RSP_ERR_ARG, "no output requested");
+    if (batch == 0) return RSP_OK;
+    const void* d_echo = nullptr;
+    int32_t d_dtype = RSP_C64;
+    rc = stage_echo(ctx, echo, dtype, layout, batch, &d_echo, &d_dtype);
+    if (rc) return rc;
+    const int64_t Ro = ctx->p.R_out;
+    const size_t cells = (size_t)batch * P * Ro;
+    if ((rc = ensure(ctx, ctx->st_rdm, cells * sizeof(float)))) return rc;
+    if (cfar) {
+        if ((rc = ensure(ctx, ctx->st_flag, cells))) return rc;
+        if ((rc = ensure(ctx, ctx->st_flagV, cells))) return rc;
+    }
+    rc = rsp_pc_mtd_cfar_dev(ctx, d_echo, d_dtype, batch, cfar, (float*)ctx->st_rdm.p,
+                             cfar ? (uint8_t*)ctx->st_flag.p : nullptr, cfar ? (uint8_t*)ctx->st_flagV.p : nullptr,
+                             ctx->stream);
+    if (rc) return rc;
+    if (rdm_out && (rc = fetch(ctx, (const float*)ctx->st_rdm.p, rdm_out, batch, P, Ro, out_layout))) return rc;
+    if (cfar) {
+        if ((rc = fetch(ctx, (const uint8_t*)ctx->st_flag.p, flag_out, batch, P, Ro, out_layout))) return rc;
+        if (flagV_out &&
+            (rc = fetch(ctx, (const uint8_t*)ctx->st_flagV.p, flagV_out, batch, P, Ro, out_layout)))
+            return rc;
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return RSP_OK;
+}
+
+int rsp_pc_mtd(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+               int64_t batch, float* rdm_out, int32_t rdm_layout) {
+    if (!rdm_out) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd: null rdm_out");
+    return rsp_pc_mtd_cfar(ctx, echo, dtype, layout, P, R, batch, nullptr, rdm_out, rdm_layout, nullptr, nullptr);
+}
+
+int rsp_cfar(rsp_ctx* ctx, const float* rdm, int32_t rdm_layout, int64_t V, int64_t R, int64_t batch,
+             const rsp_cfar_params* cfar, uint8_t* flag_out, uint8_t* flagV_out) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "null ctx");
+    if (!rdm || !cfar || !flag_out || V < 1 || R < 1 || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_cfar: bad argument");
+    if (rdm_layout != RSP_ROWMAJOR && rdm_layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad rdm_layout");
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    const size_t cells = (size_t)batch * V * R;
+    int rc;
+    if ((rc = ensure(ctx, ctx->st_in, cells * sizeof(float)))) return rc;
+    if ((rc = ensure(ctx, ctx->st_rdm, cells * sizeof(float)))) return rc;
+    if ((rc = ensure(ctx, ctx->st_flag, cells))) return rc;
+    if ((rc = ensure(ctx, ctx->st_flagV, cells))) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->st_in.p, rdm, cells * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    const float* d_rdm = (const float*)ctx->st_in.p;
+    if (rdm_layout == RSP_COLMAJOR) {  // MATLAB V x R = [b][R][V] -> [b][V][R]
+        HIP_TRY(ctx, rsp::launch_transpose_f32(d_rdm, (float*)ctx->st_rdm.p, batch, (int)R, (int)V, ctx->stream));
+        d_rdm = (const float*)ctx->st_rdm.p;
+    }
+    rc = rsp_cfar_dev(ctx, d_rdm, V, R, batch, cfar, (uint8_t*)ctx->st_flag.p, (uint8_t*)ctx->st_flagV.p, ctx->stream);
+    if (rc) return rc;
+    if ((rc = fetch(ctx, (const uint8_t*)ctx->st_flag.p, flag_out, batch, V, R, rdm_layout))) return rc;
+    if (flagV_out && (rc = fetch(ctx, (const uint8_t*)ctx->st_flagV.p, flagV_out, batch, V, R, rdm_layout)))
+        return rc;
+    return RSP_OK;
+}
+

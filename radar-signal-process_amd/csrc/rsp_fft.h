@@ -1,0 +1,195 @@
+// rsp_fft.h -- in-LDS mixed-radix Stockham FFT building blocks for gfx950.
+//
+// A length-N complex fp32 FFT lives in one LDS array (float2, one pad slot per 16
+// elements so the stride-R scatter of a radix-R pass is bank-conflict free).  Each pass
+// is the autosorting Stockham DIT step (Govindaraju et al., SC'08):
+//     for butterfly j < N/R:  v[r] = buf[j + r*N/R] * W_{Ns*R}^{r*(j%Ns)};  v = DFT_R(v);
+//                             buf[(j/Ns)*Ns*R + j%Ns + r*Ns] = v[r]
+// done in place: every thread reads its R inputs to registers, a barrier, then writes.
+// The radix plan is chosen at compile time (largest of 16/8/4/2 with N/R >= the threads
+// working on one transform, radix 3 for the 3*2^k sizes), so every index division is by
+// a compile-time constant.  Twiddles come from a per-N fp32 table W_N^e built in fp64 on
+// the host (accurate to 0.5 ulp), read through the vector L1/L2.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rsp {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// a * (-j)
+__device__ __forceinline__ float2 cmul_mj(float2 a) { return make_float2(a.y, -a.x); }
+
+// LDS index with one pad slot per 16 elements.
+__host__ __device__ constexpr int pidx(int i) { return i + (i >> 4); }
+__host__ __device__ constexpr int padded_len(int n) { return n + (n >> 4) + 1; }
+
+// ---------------------------------------------------------------- register DFTs (forward)
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+    float2 t = a;
+    a = cadd(t, b);
+    b = csub(t, b);
+}
+
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    float2 t2 = cadd(a1, a3), t3 = cmul_mj(csub(a1, a3));
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = cadd(t1, t3);
+    a3 = csub(t1, t3);
+}
+
+__device__ __forceinline__ void dft3(float2& a0, float2& a1, float2& a2) {
+    const float s = 0.86602540378443864676f;  // sqrt(3)/2
+    float2 t = cadd(a1, a2);
+    float2 d = csub(a1, a2);
+    float2 m = make_float2(a0.x - 0.5f * t.x, a0.y - 0.5f * t.y);
+    a0 = cadd(a0, t);
+    // X1 = m - j*s*d ; X2 = m + j*s*d
+    float2 jd = make_float2(-s * d.y, s * d.x);  // j*s*d
+    a1 = csub(m, jd);
+    a2 = cadd(m, jd);
+}
+
+__device__ __forceinline__ void dft8(float2* v) {
+    const float h = 0.70710678118654752440f;
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    dft4(e0, e1, e2, e3);
+    dft4(o0, o1, o2, o3);
+    // o_k *= W8^k
+    o1 = make_float2(h * (o1.x + o1.y), h * (o1.y - o1.x));
+    o2 = cmul_mj(o2);
+    o3 = make_float2(h * (o3.y - o3.x), -h * (o3.x + o3.y));
+    v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
+    v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
+    v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
+    v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
+}
+
+__device__ __forceinline__ void dft16(float2* v) {
+    // n = 4*n1 + n2, k = k1 + 4*k2
+    const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+    const float h = 0.70710678118654752440f;
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+    // v[4*k1 + n2] now holds b[n2][k1]; multiply by W16^(n2*k1)
+    // n2=1: k1=1..3 -> W^1, W^2, W^3 ; n2=2: W^2, W^4, W^6 ; n2=3: W^3, W^6, W^9
+    v[5] = cmul(v[5], make_float2(c1, -s1));
+    v[9] = make_float2(h * (v[9].x + v[9].y), h * (v[9].y - v[9].x));
+    v[13] = cmul(v[13], make_float2(s1, -c1));
+    v[6] = make_float2(h * (v[6].x + v[6].y), h * (v[6].y - v[6].x));
+    v[10] = cmul_mj(v[10]);
+    v[14] = make_float2(h * (v[14].y - v[14].x), -h * (v[14].x + v[14].y));
+    v[7] = cmul(v[7], make_float2(s1, -c1));
+    v[11] = make_float2(h * (v[11].y - v[11].x), -h * (v[11].x + v[11].y));
+    v[15] = cmul(v[15], make_float2(-c1, s1));
+    // second stage: for each k1, DFT4 over n2 of v[4*k1 + n2] -> X[k1 + 4*k2]
+    float2 x[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        float2 a0 = v[4 * k1 + 0], a1 = v[4 * k1 + 1], a2 = v[4 * k1 + 2], a3 = v[4 * k1 + 3];
+        dft4(a0, a1, a2, a3);
+        x[k1] = a0; x[k1 + 4] = a1; x[k1 + 8] = a2; x[k1 + 12] = a3;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = x[i];
+}
+
+template <int R>
+__device__ __forceinline__ void dft(float2* v) {
+    if constexpr (R == 2) {
+        dft2(v[0], v[1]);
+    } else if constexpr (R == 3) {
+        dft3(v[0], v[1], v[2]);
+    } else if constexpr (R == 4) {
+        dft4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (R == 8) {
+        dft8(v);
+    } else if constexpr (R == 16) {
+        dft16(v);
+    } else {
+        static_assert(R == 2, "unsupported radix");
+    }
+}
+
+// ---------------------------------------------------------------- plan + passes
+__host__ __device__ constexpr int pick_radix(int rem, int n, int g) {
+    // prefer the largest power-of-two radix that keeps every working thread busy
+    if (rem % 16 == 0 && n / 16 >= g) return 16;
+    if (rem % 8 == 0 && n / 8 >= g) return 8;
+    if (rem % 4 == 0 && n / 4 >= g) return 4;
+    if (rem % 16 == 0) return 16;
+    if (rem % 8 == 0) return 8;
+    if (rem % 4 == 0) return 4;
+    if (rem % 2 == 0) return 2;
+    if (rem % 3 == 0) return 3;
+    return rem;
+}
+
+__host__ __device__ constexpr bool fft_size_ok(int n) {
+    if (n < 2) return false;
+    while (n % 2 == 0) n /= 2;
+    return n == 1 || n == 3;
+}
+
+// One Stockham pass.  G threads (t = 0..G-1) work on this transform; other threads of the
+// block must call with t >= G so the barriers stay uniform.
+template <int N, int R, int G, int Ns>
+__device__ __forceinline__ void fft_pass(float2* buf, int t, const float2* __restrict__ tw) {
+    constexpr int NB = N / R;
+    constexpr int PER = (NB + G - 1) / G;
+    float2 v[PER][R];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int j = t + i * G;
+        if (t < G && j < NB) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[i][r] = buf[pidx(j + r * NB)];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int j = t + i * G;
+        if (t < G && j < NB) {
+            const int k = j % Ns;
+            if constexpr (Ns > 1) {
+                constexpr int STRIDE = N / (Ns * R);
+                const int e = k * STRIDE;
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[i][r] = cmul(v[i][r], tw[r * e]);
+            }
+            dft<R>(v[i]);
+            const int idxD = (j / Ns) * Ns * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[pidx(idxD + r * Ns)] = v[i][r];
+        }
+    }
+    __syncthreads();
+}
+
+template <int N, int G, int Ns>
+__device__ __forceinline__ void fft_rec(float2* buf, int t, const float2* __restrict__ tw) {
+    if constexpr (Ns < N) {
+        constexpr int R = pick_radix(N / Ns, N, G);
+        static_assert(R == 2 || R == 3 || R == 4 || R == 8 || R == 16, "FFT size must be 2^k or 3*2^k");
+        fft_pass<N, R, G, Ns>(buf, t, tw);
+        fft_rec<N, G, Ns * R>(buf, t, tw);
+    }
+}
+
+// Forward FFT (e^{-i}) of buf[pidx(0..N-1)], natural order in and out, in place.
+// Every thread of the block must call it (it contains barriers).
+template <int N, int G>
+__device__ __forceinline__ void fft_lds(float2* buf, int t, const float2* __restrict__ tw) {
+    fft_rec<N, G, 1>(buf, t, tw);
+}
+
+}  // namespace rsp

@@ -1,0 +1,90 @@
+// rsp_internal.h -- argument blocks shared by the C-ABI host code (rsp_capi.cpp) and the
+// HIP kernels (rsp_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rsp.h"
+
+namespace rsp {
+
+constexpr int kBlock = 256;  // threads per workgroup for every kernel (4 waves of 64)
+
+// One pulse-compression segment as the kernel sees it (see rsp_pc_segment).
+struct SegDev {
+    int kind;        // RSP_SEG_FIR / RSP_SEG_MF
+    int fir_shift;
+    int in_start, in_len;
+    int out_start, out_len;
+    int nfft;
+    int ntaps;
+    float scale;
+    const float2* H;   // MF: conj(FFT_nfft(scale*replica)) / nfft
+    const float2* tw;  // MF: W_nfft^e table, e < nfft
+    float taps[RSP_MAX_FIR_TAPS];
+};
+
+struct PcArgs {
+    int P, R, R_out;
+    int nseg;
+    int nzero;                          // output column ranges no segment writes
+    int zero_lo[RSP_MAX_SEG + 1];
+    int zero_hi[RSP_MAX_SEG + 1];
+    SegDev seg[RSP_MAX_SEG];
+};
+
+// Doppler-dimension CFAR on one column tile (Function_CFAR1D_sub on used.').
+struct CfarVArgs {
+    int enabled;
+    int lo, hi;          // used rows [lo, hi) = rows M0+2 .. V-M0 (1-based)
+    int ref, save, method;
+    float T;
+    int cz_lo, cz_hi;    // rows zeroed before CFAR (main_cfar.m:90-91), empty if lo >= hi
+    int nseg;            // column segments (fun_CFARflag); columns outside get flag 0
+    int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
+};
+
+struct MtdArgs {
+    int P, R_out;
+    int shift;           // fftshift offset floor(P/2), or 0
+    int z_lo, z_hi;      // fun_0v_pressing rows zeroed in the RDM
+    const float* win;    // slow-time window, P entries
+    const float2* tw;    // W_P^e table
+    CfarVArgs cv;
+};
+
+// Range-dimension CFAR at the Doppler hits (executeCFAR.m:35-89).
+struct CfarRArgs {
+    int V, R;
+    int lo, hi;          // used rows
+    int rflag;
+    int ref, save, method;
+    float T;
+    int cz_lo, cz_hi;    // rows zeroed before CFAR
+    int nseg;
+    int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
+};
+
+bool mtd_size_supported(int P);
+bool pc_nfft_supported(int n);
+size_t pc_lds_bytes(int max_nfft);
+
+hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, const PcArgs& a,
+                     size_t lds_bytes, hipStream_t s);
+hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
+                      hipStream_t s);
+// Doppler CFAR straight from an RDM ([ncpi][V][R] fp32) for rsp_cfar.
+hipError_t launch_cfar_v(const float* rdm, uint8_t* flagV, int ncpi, int V, int R,
+                         const CfarVArgs& a, hipStream_t s);
+hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
+                         const CfarRArgs& a, hipStream_t s);
+// dtype/layout conversion of a host-API input into [batch][P][R] complex float32.
+hipError_t launch_ingest(const void* in, int dtype, int layout, float2* out, int64_t batch,
+                         int P, int R, hipStream_t s);
+// [batch][A][B] -> [batch][B][A] for 4-byte and 1-byte elements.
+hipError_t launch_transpose_f32(const float* in, float* out, int64_t batch, int A, int B,
+                                hipStream_t s);
+hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, int A, int B,
+                               hipStream_t s);
+
+}  // namespace rsp

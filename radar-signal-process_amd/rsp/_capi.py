@@ -1,0 +1,114 @@
+"""ctypes binding of the C ABI declared in include/rsp.h (lib/librsp.so).
+
+The shared library is the product: every PC / MTD / CFAR computation runs in its
+gfx950 kernels.  There is no CPU fallback -- if the library (or a GPU) is missing,
+the calls raise.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librsp.so")
+
+RSP_MAX_SEG = 4
+RSP_MAX_FIR_TAPS = 64
+
+# rsp_status
+RSP_OK, RSP_ERR_ARG, RSP_ERR_SHAPE, RSP_ERR_UNSUPPORTED, RSP_ERR_CFAR_WINDOW, RSP_ERR_HIP, RSP_ERR_NOMEM = range(7)
+# rsp_dtype
+RSP_C64, RSP_C128, RSP_C32F16 = 0, 1, 2
+# rsp_layout
+RSP_ROWMAJOR, RSP_COLMAJOR = 0, 1
+# rsp_seg_kind
+RSP_SEG_FIR, RSP_SEG_MF = 0, 1
+# rsp_window
+RSP_WIN_KAISER, RSP_WIN_HAMMING, RSP_WIN_RECT = 0, 1, 2
+
+# Every exported symbol of include/rsp.h (checked by tests/test_capi_cpu.py)
+EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_set_chunk",
+           "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
+           "rsp_pc_dev", "rsp_profile", "rsp_profile_read")
+RSP_NKERNELS = 4
+KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
+
+
+class RspError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("rsp error %d: %s" % (code, msg))
+        self.code = code
+
+
+class rsp_pc_segment(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("fir_shift", C.c_int32),
+                ("in_start", C.c_int64), ("in_len", C.c_int64),
+                ("out_start", C.c_int64), ("out_len", C.c_int64),
+                ("nfft", C.c_int64), ("scale", C.c_double),
+                ("coef_len", C.c_int64),
+                ("coef_re", C.POINTER(C.c_double)), ("coef_im", C.POINTER(C.c_double))]
+
+
+class rsp_params(C.Structure):
+    _fields_ = [("P", C.c_int64), ("R", C.c_int64), ("R_out", C.c_int64),
+                ("nseg", C.c_int32), ("window", C.c_int32), ("window_beta", C.c_double),
+                ("fftshift", C.c_int32), ("zero_v_div", C.c_int32),
+                ("seg", rsp_pc_segment * RSP_MAX_SEG)]
+
+
+class rsp_cfar_params(C.Structure):
+    _fields_ = [("refR", C.c_int32), ("saveR", C.c_int32), ("methodR", C.c_int32), ("TR", C.c_double),
+                ("refV", C.c_int32), ("saveV", C.c_int32), ("methodV", C.c_int32), ("TV", C.c_double),
+                ("M0", C.c_int32), ("rFlag", C.c_int32), ("zero_v_div", C.c_int32),
+                ("nseg", C.c_int32),
+                ("seg_lo", C.c_int64 * RSP_MAX_SEG), ("seg_hi", C.c_int64 * RSP_MAX_SEG)]
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load librsp.so (raises OSError if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError("librsp.so not found at %s -- build it with `make -C radar-signal-process_amd` "
+                      "or __graft_entry__.build()" % p)
+    lib = C.CDLL(p)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    lib.rsp_version.restype = C.c_char_p
+    lib.rsp_version.argtypes = []
+    lib.rsp_last_error.restype = C.c_char_p
+    lib.rsp_last_error.argtypes = [vp]
+    lib.rsp_create.restype = C.c_int
+    lib.rsp_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(rsp_params)]
+    lib.rsp_destroy.restype = C.c_int
+    lib.rsp_destroy.argtypes = [vp]
+    lib.rsp_set_chunk.restype = C.c_int
+    lib.rsp_set_chunk.argtypes = [vp, i64]
+    lib.rsp_pc_mtd.restype = C.c_int
+    lib.rsp_pc_mtd.argtypes = [vp, vp, i32, i32, i64, i64, i64, vp, i32]
+    lib.rsp_cfar.restype = C.c_int
+    lib.rsp_cfar.argtypes = [vp, vp, i32, i64, i64, i64, C.POINTER(rsp_cfar_params), vp, vp]
+    lib.rsp_pc_mtd_cfar.restype = C.c_int
+    lib.rsp_pc_mtd_cfar.argtypes = [vp, vp, i32, i32, i64, i64, i64, C.POINTER(rsp_cfar_params),
+                                    vp, i32, vp, vp]
+    lib.rsp_pc_mtd_cfar_dev.restype = C.c_int
+    lib.rsp_pc_mtd_cfar_dev.argtypes = [vp, vp, i32, i64, C.POINTER(rsp_cfar_params), vp, vp, vp, vp]
+    lib.rsp_cfar_dev.restype = C.c_int
+    lib.rsp_cfar_dev.argtypes = [vp, vp, i64, i64, i64, C.POINTER(rsp_cfar_params), vp, vp, vp]
+    lib.rsp_pc_dev.restype = C.c_int
+    lib.rsp_pc_dev.argtypes = [vp, vp, i32, i64, vp, vp]
+    lib.rsp_profile.restype = C.c_int
+    lib.rsp_profile.argtypes = [vp, i32]
+    lib.rsp_profile_read.restype = C.c_int
+    lib.rsp_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    _lib = lib
+    return lib
+
+
+def check(rc, ctx=None):
+    if rc != RSP_OK:
+        lib = load_library()
+        msg = lib.rsp_last_error(ctx)
+        raise RspError(rc, msg.decode() if msg else "")

@@ -1,0 +1,194 @@
+"""Engine: one rsp_ctx (one device, one parameter set) behind a Python object.
+
+Host-buffer methods take/return numpy arrays and go through the synchronous C entry
+points (the MEX path).  Device methods take torch tensors that already live on the GPU
+and enqueue on the current torch stream (the benchmark path); torch is only used for
+device memory and streams here -- all arithmetic happens in librsp's kernels.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _capi as capi
+from . import presets
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Engine:
+    def __init__(self, spec, device=0, chunk=0):
+        self.spec = spec
+        self.lib = capi.load_library()
+        prm, self._keep = spec.to_c()
+        ctx = C.c_void_p()
+        rc = self.lib.rsp_create(C.byref(ctx), int(device), C.byref(prm))
+        capi.check(rc, None)
+        self.ctx = ctx
+        self.device = device
+        if chunk:
+            self.set_chunk(chunk)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.rsp_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_chunk(self, cpis):
+        capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)
+
+    @property
+    def shape(self):
+        return self.spec.P, self.spec.R_out
+
+    # ------------------------------------------------------------------ host buffers
+    @staticmethod
+    def _echo_host(echo, layout):
+        a = np.asarray(echo)
+        if a.dtype == np.complex128:
+            dt = capi.RSP_C128
+        elif a.dtype == np.complex64:
+            dt = capi.RSP_C64
+        elif a.dtype == np.float16 and a.shape[-1] == 2:
+            dt = capi.RSP_C32F16   # [..., 2] interleaved I/Q pairs
+        else:
+            a = a.astype(np.complex128)
+            dt = capi.RSP_C128
+        return np.ascontiguousarray(a), dt
+
+    def _batch_dims(self, echo_shape, layout):
+        P, R = self.spec.P, self.spec.R
+        if layout == capi.RSP_COLMAJOR:
+            # MATLAB P x R column-major arrives as numpy [..., R, P] C order
+            tail = (R, P)
+        else:
+            tail = (P, R)
+        if tuple(echo_shape[-2:]) != tail:
+            raise ValueError("echo shape %s does not end in %s" % (echo_shape, tail))
+        return int(np.prod(echo_shape[:-2])) if len(echo_shape) > 2 else 1
+
+    def pc_mtd_cfar(self, echo, cfar=None, layout=capi.RSP_ROWMAJOR, out_layout=capi.RSP_ROWMAJOR,
+                    want_flagV=True):
+        """echo: [batch][P][R] complex (row-major) or MATLAB [batch][R][P] with layout=COLMAJOR.
+        Returns rdm (float32) [, flag, flagV (uint8)] in out_layout."""
+        a, dt = self._echo_host(echo, layout)
+        shape = a.shape if dt != capi.RSP_C32F16 else a.shape[:-1]
+        batch = self._batch_dims(shape, layout)
+        P, Ro = self.spec.P, self.spec.R_out
+        oshape = (batch, P, Ro) if out_layout == capi.RSP_ROWMAJOR else (batch, Ro, P)
+        rdm = np.empty(oshape, np.float32)
+        flag = flagV = None
+        cp = None
+        if cfar is not None:
+            cp = cfar.to_c()
+            flag = np.empty(oshape, np.uint8)
+            flagV = np.empty(oshape, np.uint8) if want_flagV else None
+        rc = self.lib.rsp_pc_mtd_cfar(self.ctx, _ptr(a), dt, layout, P, self.spec.R, batch,
+                                      C.byref(cp) if cp is not None else None, _ptr(rdm), out_layout,
+                                      _ptr(flag), _ptr(flagV))
+        capi.check(rc, self.ctx)
+        if cfar is None:
+            return rdm
+        return rdm, flag, flagV
+
+    def pc_mtd(self, echo, layout=capi.RSP_ROWMAJOR, out_layout=capi.RSP_ROWMAJOR):
+        return self.pc_mtd_cfar(echo, None, layout, out_layout)
+
+    def cfar(self, rdm, cfar, layout=capi.RSP_ROWMAJOR):
+        """rdm: [batch][V][R] float (or MATLAB [batch][R][V] with COLMAJOR).  -> flag, flagV."""
+        r = np.ascontiguousarray(rdm, dtype=np.float32)
+        if r.ndim == 2:
+            r = r[None]
+        batch = r.shape[0]
+        V, R = (r.shape[1], r.shape[2]) if layout == capi.RSP_ROWMAJOR else (r.shape[2], r.shape[1])
+        flag = np.empty(r.shape, np.uint8)
+        flagV = np.empty(r.shape, np.uint8)
+        cp = cfar.to_c()
+        rc = self.lib.rsp_cfar(self.ctx, _ptr(r), layout, V, R, batch, C.byref(cp), _ptr(flag), _ptr(flagV))
+        capi.check(rc, self.ctx)
+        return flag, flagV
+
+    # ------------------------------------------------------------------ device tensors
+    @staticmethod
+    def _stream_handle(stream):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return C.c_void_p(s.cuda_stream)
+
+    def run_dev(self, echo, rdm=None, flag=None, flagV=None, cfar=None, stream=None):
+        """echo: torch tensor [batch, P, R] complex64, or [batch, P, R, 2] float16 (I/Q).
+        rdm [batch, P, R_out] float32, flag / flagV uint8 of the same shape (flagV optional).
+        Asynchronous on `stream` (default: torch's current stream)."""
+        import torch
+        if not echo.is_cuda or not echo.is_contiguous():
+            raise ValueError("echo must be a contiguous CUDA tensor")
+        if echo.dtype == torch.complex64:
+            dt, batch = capi.RSP_C64, echo.shape[0]
+            tail = tuple(echo.shape[1:])
+        elif echo.dtype == torch.float16:
+            dt, batch = capi.RSP_C32F16, echo.shape[0]
+            tail = tuple(echo.shape[1:3])
+            if echo.shape[-1] != 2:
+                raise ValueError("fp16 echo must be [batch, P, R, 2]")
+        else:
+            raise ValueError("echo dtype must be complex64 or float16 I/Q")
+        if tail != (self.spec.P, self.spec.R):
+            raise ValueError("echo is %s, engine expects [batch, %d, %d]" % (tuple(echo.shape), self.spec.P, self.spec.R))
+        want = (batch, self.spec.P, self.spec.R_out)
+        for t, dtp in ((rdm, torch.float32), (flag, torch.uint8), (flagV, torch.uint8)):
+            if t is not None and (tuple(t.shape) != want or t.dtype != dtp or not t.is_contiguous() or not t.is_cuda):
+                raise ValueError("output tensor must be contiguous CUDA %s of shape %s" % (dtp, want))
+        cp = cfar.to_c() if cfar is not None else None
+        rc = self.lib.rsp_pc_mtd_cfar_dev(
+            self.ctx, C.c_void_p(echo.data_ptr()), dt, batch, C.byref(cp) if cp is not None else None,
+            C.c_void_p(rdm.data_ptr()) if rdm is not None else None,
+            C.c_void_p(flag.data_ptr()) if flag is not None else None,
+            C.c_void_p(flagV.data_ptr()) if flagV is not None else None,
+            self._stream_handle(stream))
+        capi.check(rc, self.ctx)
+
+    def pc_dev(self, echo, out, stream=None):
+        """Pulse compression alone: out [batch, P, R_out] complex64."""
+        import torch
+        dt = capi.RSP_C64 if echo.dtype == torch.complex64 else capi.RSP_C32F16
+        rc = self.lib.rsp_pc_dev(self.ctx, C.c_void_p(echo.data_ptr()), dt, echo.shape[0],
+                                 C.c_void_p(out.data_ptr()), self._stream_handle(stream))
+        capi.check(rc, self.ctx)
+
+    def profile(self, enable=True):
+        """Start (and reset) or stop per-kernel HIP-event timing inside librsp."""
+        capi.check(self.lib.rsp_profile(self.ctx, 1 if enable else 0), self.ctx)
+
+    def profile_read(self):
+        """{kernel name: (total ms, launches)} since profile(True)."""
+        ms = (C.c_double * capi.RSP_NKERNELS)()
+        n = (C.c_int64 * capi.RSP_NKERNELS)()
+        capi.check(self.lib.rsp_profile_read(self.ctx, ms, n), self.ctx)
+        return {capi.KERNEL_NAMES[k]: (ms[k], n[k]) for k in range(capi.RSP_NKERNELS) if n[k]}
+
+    def cfar_dev(self, rdm, flag, flagV=None, cfar=None, stream=None):
+        b, V, R = rdm.shape
+        cp = cfar.to_c()
+        rc = self.lib.rsp_cfar_dev(self.ctx, C.c_void_p(rdm.data_ptr()), V, R, b, C.byref(cp),
+                                   C.c_void_p(flag.data_ptr()),
+                                   C.c_void_p(flagV.data_ptr()) if flagV is not None else None,
+                                   self._stream_handle(stream))
+        capi.check(rc, self.ctx)
+
+
+def engine_for(name, P, R, device=0, chunk=0):
+    return Engine(presets.make(name, P, R), device=device, chunk=chunk)

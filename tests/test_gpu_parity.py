@@ -1,0 +1,268 @@
+"""GPU parity of the HIP product path (through the C ABI) against the fp64 oracles.
+
+Bars (written here): RDM rel-err <= 1e-5 (Frobenius) vs the fp64 oracle on
+the same synthetic echo; CFAR flags identical except cells whose oracle decision is within
+1e-5 relative of its threshold ("near-threshold", counted, bounded).  Integer/index work
+(layouts, batching, chunking) must be bit-exact.
+"""
+import numpy as np
+import pytest
+
+import rsp_ref as ref
+from _util import NEAR_TOL, RDM_TOL, flag_mismatch, oracle_flags, oracle_rdm, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _engine(name, P, R, chunk=0):
+    from rsp import presets
+    from rsp.engine import Engine
+    return Engine(presets.make(name, P, R), device=0, chunk=chunk)
+
+
+def _echo(eng, batch, seed=1001):
+    from rsp import synth
+    return synth.echo_numpy(eng.spec, batch, seed=seed)
+
+
+# ---------------------------------------------------------------- pulse compression alone
+@pytest.mark.parametrize("name,P,R", [("v2", 64, 1024), ("v2", 128, 4096), ("dmx", 64, 4096), ("legacy", 48, 1031)])
+def test_pc_parity(torch_cuda, name, P, R):
+    torch = torch_cuda
+    eng = _engine(name, P, R)
+    echo = _echo(eng, 2)
+    d_in = torch.from_numpy(echo).cuda()
+    d_pc = torch.empty((2, P, R), dtype=torch.complex64, device="cuda")
+    eng.pc_dev(d_in, d_pc)
+    torch.cuda.synchronize()
+    got = d_pc.cpu().numpy()
+    e64 = echo.astype(np.complex128)
+    for b in range(2):
+        if name == "v2":
+            rp = ref.v2_params(P, R)
+            _, p2, p3 = ref.v2_pulses(rp)
+            want = ref.fun_lss_pulse_compression(e64[b], p2, p3, 228, 723, R - 951, fir_shift=True)
+        elif name == "legacy":
+            from rsp import presets
+            want = ref.fun_lss_pulse_compression(e64[b], presets.load_data("legacy_pulse2"),
+                                                 presets.load_data("legacy_pulse3"), 82, 242, R - 324,
+                                                 fir_shift=False, offset2=75, offset3=160)
+        else:
+            from rsp import presets
+            H = ref.dmx_matched_filter(presets.load_data("refDDCDataMF1"), R)
+            want = ref.dmx_pulse_compression(e64[b:b + 1], 0, R, H)[0]
+        err = np.linalg.norm(got[b] - want) / np.linalg.norm(want)
+        assert err < RDM_TOL, (name, b, err)
+
+
+# ---------------------------------------------------------------- PC -> MTD -> 0-v
+@pytest.mark.parametrize("name,P,R,batch", [("v2", 64, 1024, 3), ("v2", 128, 4096, 4), ("dmx", 128, 4096, 2),
+                                            ("v2", 256, 8192, 2), ("v2", 512, 16384, 1), ("legacy", 96, 1031, 2),
+                                            ("dmx", 32, 512, 3)])
+def test_pc_mtd_parity(torch_cuda, name, P, R, batch):
+    torch = torch_cuda
+    eng = _engine(name, P, R)
+    echo = _echo(eng, batch)
+    d_in = torch.from_numpy(echo).cuda()
+    d_rdm = torch.empty((batch, P, R), dtype=torch.float32, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm)
+    torch.cuda.synchronize()
+    got = d_rdm.cpu().numpy()
+    want = oracle_rdm(name, echo)
+    err = rel_err(got, want)
+    assert err < RDM_TOL, err
+    # the zero-velocity rows are exactly zero
+    lo, hi = ref.zero_v_rows(P, 150)
+    assert np.all(got[:, lo:hi, :] == 0)
+
+
+# ---------------------------------------------------------------- full chain with CFAR
+@pytest.mark.parametrize("name,P,R,batch", [("v2", 64, 1024, 2), ("v2", 128, 4096, 3), ("dmx", 128, 4096, 2),
+                                            ("legacy", 96, 1031, 1)])
+def test_chain_cfar_parity(torch_cuda, name, P, R, batch):
+    torch = torch_cuda
+    from rsp import presets
+    eng = _engine(name, P, R)
+    cf = presets.default_cfar(eng.spec)
+    echo = _echo(eng, batch)
+    d_in = torch.from_numpy(echo).cuda()
+    shp = (batch, P, R)
+    d_rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    d_fv = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm, flag=d_flag, flagV=d_fv, cfar=cf)
+    torch.cuda.synchronize()
+    rdm = oracle_rdm(name, echo)
+    assert rel_err(d_rdm.cpu().numpy(), rdm) < RDM_TOL
+    flag, flagV, amb = oracle_flags(rdm, cf)
+    hard, soft = flag_mismatch(d_flag.cpu().numpy(), flag, amb)
+    hardv, softv = flag_mismatch(d_fv.cpu().numpy(), flagV, amb)
+    assert hard == 0 and hardv == 0, (hard, hardv)
+    assert soft <= max(2, flag.size // 100000) and softv <= max(2, flag.size // 100000), (soft, softv)
+    assert flag.sum() > 0 and flagV.sum() > flag.sum()
+
+
+def test_cfar_standalone_matches_oracle(torch_cuda):
+    """rsp_cfar (executeCFAR / fun_CFARflag) on a given RDM: same input for both sides."""
+    from rsp import presets
+    from rsp.engine import Engine
+    rng = np.random.default_rng(3)
+    V, R = 128, 868
+    rdm = np.abs(rng.standard_normal((2, V, R)) + 1j * rng.standard_normal((2, V, R))).astype(np.float32)
+    rdm[:, 40, 100] = 40.0
+    rdm[:, 41, 100] = 30.0
+    rdm[:, 90, 500:503] = [20.0, 25.0, 22.0]
+    cf = presets.Cfar(TR=4.0, TV=4.0, M0=5, zero_v_div=20, segments=[(0, 82), (82, 318), (318, 868)])
+    eng = Engine(presets.dmx(16, 64))
+    flag, flagV = eng.cfar(rdm, cf)
+    want, wantV, amb = oracle_flags(rdm.astype(np.float64), cf)
+    assert flag_mismatch(flag, want, amb)[0] == 0
+    assert flag_mismatch(flagV, wantV, amb)[0] == 0
+    assert want[:, 40, 100].all() and want.sum() > 2
+
+
+# ---------------------------------------------------------------- boundary behaviour
+def test_host_api_matlab_layout_and_dtypes(torch_cuda):
+    """rsp_pc_mtd_cfar host path: MATLAB column-major complex double in, column-major out;
+    identical to the row-major complex64 device path (conversion is exact)."""
+    torch = torch_cuda
+    from rsp import _capi as capi, presets
+    eng = _engine("v2", 64, 1024)
+    cf = presets.default_cfar(eng.spec)
+    echo = _echo(eng, 2)
+    rdm_r, flag_r, fv_r = eng.pc_mtd_cfar(echo, cf)                       # complex64 row-major
+    col = np.ascontiguousarray(np.swapaxes(echo.astype(np.complex128), 1, 2))   # [b][R][P]
+    rdm_c, flag_c, fv_c = eng.pc_mtd_cfar(col, cf, layout=capi.RSP_COLMAJOR, out_layout=capi.RSP_COLMAJOR)
+    np.testing.assert_array_equal(np.swapaxes(rdm_c, 1, 2), rdm_r)
+    np.testing.assert_array_equal(np.swapaxes(flag_c, 1, 2), flag_r)
+    np.testing.assert_array_equal(np.swapaxes(fv_c, 1, 2), fv_r)
+    d_in = torch.from_numpy(echo).cuda()
+    d_rdm = torch.empty((2, 64, 1024), dtype=torch.float32, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_rdm.cpu().numpy(), rdm_r)
+
+
+def test_fp16_input_parity(torch_cuda):
+    """fp16 I/Q storage, fp32 compute: parity against the oracle fed the same fp16 samples."""
+    torch = torch_cuda
+    from rsp import synth
+    eng = _engine("v2", 128, 4096)
+    echo = _echo(eng, 2)
+    half = synth.to_half_iq(echo)
+    d_in = torch.from_numpy(half).cuda()
+    d_rdm = torch.empty((2, 128, 4096), dtype=torch.float32, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm)
+    torch.cuda.synchronize()
+    e16 = half[..., 0].astype(np.float64) + 1j * half[..., 1].astype(np.float64)
+    assert rel_err(d_rdm.cpu().numpy(), oracle_rdm("v2", e16)) < RDM_TOL
+
+
+def test_batch_and_chunk_invariance(torch_cuda):
+    """A CPI's outputs do not depend on its batch neighbours or on the chunk size (bit-exact)."""
+    torch = torch_cuda
+    from rsp import presets
+    spec = presets.v2(128, 4096)
+    cf = presets.default_cfar(spec)
+    from rsp.engine import Engine
+    from rsp import synth
+    echo = synth.echo_numpy(spec, 7, seed=77)
+    d_in = torch.from_numpy(echo).cuda()
+    outs = []
+    for chunk in (1, 3, 7):
+        eng = Engine(spec, chunk=chunk)
+        r = torch.empty((7, 128, 4096), dtype=torch.float32, device="cuda")
+        f = torch.empty((7, 128, 4096), dtype=torch.uint8, device="cuda")
+        eng.run_dev(d_in, rdm=r, flag=f, cfar=cf)
+        torch.cuda.synchronize()
+        outs.append((r.cpu().numpy(), f.cpu().numpy()))
+        eng.close()
+    for r, f in outs[1:]:
+        np.testing.assert_array_equal(r, outs[0][0])
+        np.testing.assert_array_equal(f, outs[0][1])
+    eng = Engine(spec)
+    r1 = torch.empty((1, 128, 4096), dtype=torch.float32, device="cuda")
+    eng.run_dev(d_in[4:5].contiguous(), rdm=r1)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r1.cpu().numpy()[0], outs[0][0][4])
+
+
+def test_matlab_mirror(torch_cuda):
+    """rsp.matlab keeps the reference's names, argument meaning and outputs."""
+    from rsp import matlab, presets, synth
+    P, R = 64, 1024
+    params = presets.radar_params(P, R)
+    spec = presets.v2(P, R)
+    echo = synth.echo_numpy(spec, 1, seed=5)[0].astype(np.complex128)
+    got = matlab.fun_MTD_produce(echo, params)
+    want = ref.fun_MTD_produce_v2(echo, ref.v2_params(P, R))
+    assert got.shape == (P, R) and got.dtype == np.float64
+    assert rel_err(got, want) < RDM_TOL
+    M0 = ref.mtd_zero_num(P, params["wavelength"], params["prf"])
+    w32 = want.astype(np.float32).astype(np.float64)
+    f, fv = matlab.executeCFAR(w32, 5, 7, 5, 0, 5, 7, 5, 0, M0, 1)
+    wf, wfv, amb = ref.executeCFAR(w32, 5, 7, 5, 0, 5, 7, 5, 0, M0, 1, near_tol=NEAR_TOL)
+    assert f.dtype == np.float64 and f.shape == (P, R)
+    assert flag_mismatch(f, wf, amb)[0] == 0 and flag_mismatch(fv, wfv, amb)[0] == 0
+    cf = matlab.fun_CFARflag(w32, 5, 7, 5, 0, 5, 7, 5, 0, M0, 1, segments=((0, 228), (228, 951), (951, 1024)))
+    wcf, _, amb2 = ref.fun_CFARflag(w32, 5, 7, 5, 0, 5, 7, 5, 0, M0, 1,
+                                    segments=((1, 228), (229, 951), (952, 1024)), near_tol=NEAR_TOL)
+    assert flag_mismatch(cf, wcf, amb2)[0] == 0
+
+
+def test_error_behaviour(torch_cuda):
+    from rsp import RspError, _capi as capi, presets
+    from rsp.engine import Engine
+    eng = _engine("v2", 64, 1024)
+    with pytest.raises(ValueError):          # echo of the wrong shape (host-side check)
+        eng.pc_mtd(np.zeros((1, 64, 1000), np.complex64))
+    a = np.zeros((1, 64, 1000), np.complex64)  # and the C ABI's own check
+    out = np.empty((1, 64, 1000), np.float32)
+    rc = eng.lib.rsp_pc_mtd(eng.ctx, a.ctypes.data, capi.RSP_C64, capi.RSP_ROWMAJOR, 64, 1000, 1,
+                            out.ctypes.data, capi.RSP_ROWMAJOR)
+    assert rc == capi.RSP_ERR_SHAPE and b"context was created" in eng.lib.rsp_last_error(eng.ctx)
+    # MATLAB raises an index error when the Doppler window does not fit: so does the ABI
+    cf = presets.Cfar(M0=20)                 # 64 - 41 = 23 Doppler cells < 24
+    with pytest.raises(RspError) as ei:
+        eng.pc_mtd_cfar(_echo(eng, 1), cf)
+    assert ei.value.code == capi.RSP_ERR_CFAR_WINDOW
+    with pytest.raises(RspError) as ei:      # unsupported Doppler FFT length
+        Engine(presets.v2(100, 1024))
+    assert ei.value.code == capi.RSP_ERR_UNSUPPORTED
+
+
+def test_full_batch_properties(torch_cuda):
+    """c3 size (128 x 4096, batch 1024): spot CPIs against the C oracle, and the exact
+    size-independent property RDM(2x) = 2 RDM(x) (power-of-two scaling is exact in fp32)."""
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    spec = presets.v2(128, 4096)
+    cf = presets.default_cfar(spec)
+    eng = Engine(spec)
+    B = 1024
+    echo = synth.echo_torch(spec, B, seed=2024)
+    rdm = torch.empty((B, 128, 4096), dtype=torch.float32, device="cuda")
+    flag = torch.empty((B, 128, 4096), dtype=torch.uint8, device="cuda")
+    eng.run_dev(echo, rdm=rdm, flag=flag, cfar=cf)
+    torch.cuda.synchronize()
+    idx = [0, 511, 1023]
+    sample = echo[idx].cpu().numpy()
+    want = oracle_rdm("v2", sample)
+    assert rel_err(rdm[idx].cpu().numpy(), want) < RDM_TOL
+    wflag, _, amb = oracle_flags(want, cf)
+    assert flag_mismatch(flag[idx].cpu().numpy(), wflag, amb)[0] == 0
+    rdm2 = torch.empty_like(rdm)
+    flag2 = torch.empty_like(flag)
+    echo.mul_(2.0)
+    eng.run_dev(echo, rdm=rdm2, flag=flag2, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(rdm2, rdm * 2.0)
+    assert torch.equal(flag2, flag)

@@ -1,0 +1,142 @@
+"""CPU tests of the oracles (oracle/rsp_ref.py numpy, oracle/rsp_oracle.c C).
+
+Pinning: the reference's one known-answer vector (kaiser_win.mat) plus oracle-independent
+known answers: PC peak at the known delay, MTD peak at the known Doppler
+bin, CFAR on a constant field = no flags, on a single spike = exactly one flag, edge
+fallbacks; and the two independent restatements agreeing with each other.
+"""
+import numpy as np
+import pytest
+
+import coracle
+import rsp_ref as ref
+
+DATA = coracle.DATA
+
+
+def test_kaiser_golden():
+    import os
+    kw = np.load(os.path.join(os.path.dirname(__file__), "golden", "kaiser_win_1536_beta8.npy"))
+    assert kw.shape == (1536,)
+    np.testing.assert_allclose(ref.kaiser(1536, 8.0), kw, rtol=0, atol=2e-15)
+
+
+def test_matlab_builtins():
+    assert ref.mround(2.5) == 3 and ref.mround(-2.5) == -3 and ref.mround(0.49) == 0
+    # pulse lengths of the v2 chirps = MATLAB colon counts (MTD/fun_MTD_produce.m:61-63)
+    p1, p2, p3 = ref.v2_pulses(ref.v2_params())
+    assert (len(p1), len(p2), len(p3)) == (4, 200, 700)
+    # round(mean(grpdelay(b))) = 17 for the 35-tap symmetric FIR
+    assert ref.grpdelay_round_mean(ref.FIR_TAPS_RAW / 511.0) == 17
+    # filter(b,1,x): causal, zero state
+    y = ref.mfilter(np.array([1.0, 2.0]), np.array([1.0, 0.0, 0.0]))
+    np.testing.assert_array_equal(y, [1.0, 2.0, 0.0])
+    # fftshift index = numpy fftshift for even and odd lengths
+    for P in (8, 9, 64, 1536):
+        x = np.arange(P)
+        np.testing.assert_array_equal(x[ref.fftshift_index(P)], np.fft.fftshift(x))
+
+
+@pytest.mark.parametrize("P,div,rows", [(64, 150, (31, 32)), (128, 150, (62, 65)), (256, 150, (125, 130)),
+                                        (512, 150, (252, 259)), (128, 20, (57, 70))])
+def test_zero_v_rows(P, div, rows):
+    # off-centre rows (1-based zv-k .. zv+k)
+    assert ref.zero_v_rows(P, div) == rows
+    m = ref.fun_0v_pressing(np.ones((P, 3)), div)
+    assert np.all(m[rows[0]:rows[1]] == 0) and m.sum() == 3 * (P - (rows[1] - rows[0]))
+
+
+def test_mtd_zero_num():
+    p = ref.v2_params()
+    assert [ref.mtd_zero_num(P, p["wavelength"], p["prf"]) for P in (64, 128, 256, 512)] == [2, 5, 11, 22]
+
+
+def test_pc_known_delay():
+    # a lone echo of pulse3 starting at column d of segment 3 compresses to a peak at d
+    P, R = 2, 4096
+    rp = ref.v2_params(P, R)
+    _, p2, p3 = ref.v2_pulses(rp)
+    echo = np.zeros((P, R), complex)
+    d = 951 + 1000
+    echo[:, d:d + 700] = p3
+    pc = ref.fun_lss_pulse_compression(echo, p2, p3, 228, 723, R - 951)
+    assert int(np.argmax(np.abs(pc[0]))) == d
+    assert abs(abs(pc[0, d]) - 700.0) < 1e-9          # |sum |s|^2| = 700
+    # the FIR segment: an impulse at n comes out centred at n (circshift by the group delay)
+    echo = np.zeros((P, R), complex)
+    echo[:, 100] = 1.0
+    pc = ref.fun_lss_pulse_compression(echo, p2, p3, 228, 723, R - 951)
+    assert int(np.argmax(np.abs(pc[0, :228]))) == 100
+
+
+def test_mtd_known_doppler():
+    P, R = 128, 8
+    k = 20                                             # Doppler bin
+    m = np.arange(P)
+    pc = np.exp(2j * np.pi * k * m / P)[:, None] * np.ones((1, R))
+    mtd = ref.fun_Process_MTD(pc)
+    # fftshift puts bin k at row k + P/2
+    assert np.all(np.argmax(mtd, axis=0) == k + P // 2)
+
+
+def test_cfar_constant_and_spike():
+    V, R = 64, 100
+    flat = np.full((V, R), 3.0)
+    f, fv = ref.executeCFAR(flat, 5, 7, 5, 0, 5, 7, 5, 0, 2, 1)
+    assert f.sum() == 0 and fv.sum() == 0
+    spike = flat.copy()
+    spike[30, 50] = 100.0
+    f, fv = ref.executeCFAR(spike, 5, 7, 5, 0, 5, 7, 5, 0, 2, 1)
+    assert f.sum() == 1 and f[30, 50] == 1 and fv[30, 50] == 1
+    # edge fallback: a spike in the first used Doppler row still detects (right window used)
+    spike = flat.copy()
+    spike[3, 50] = 100.0                               # used rows start at M0+1 = 3
+    f, fv = ref.executeCFAR(spike, 5, 7, 5, 0, 5, 7, 5, 0, 2, 1)
+    assert f[3, 50] == 1 and f.sum() == 1
+    # range re-localisation: a Doppler hit moves to the larger neighbour that passes
+    row = flat.copy()
+    row[30, 50] = 100.0
+    row[30, 51] = 200.0
+    f, fv = ref.executeCFAR(row, 5, 7, 5, 0, 5, 7, 5, 0, 2, 1)
+    assert fv[30, 50] == 1 and fv[30, 51] == 1 and f.sum() == 1 and f[30, 51] == 1
+    # too few Doppler cells: MATLAB raises an index error
+    with pytest.raises(ref.CfarConfigError):
+        ref.executeCFAR(np.ones((20, 40)), 5, 7, 5, 0, 5, 7, 5, 0, 0, 1)
+
+
+def test_dmx_equivalence():
+    # circular correlation via FFT = direct sum with wrap (DMX_SignalProcessing_main_xzr.m:348-352)
+    rng = np.random.default_rng(0)
+    N = 256
+    x = rng.standard_normal((1, N)) + 1j * rng.standard_normal((1, N))
+    s = rng.standard_normal(20) + 1j * rng.standard_normal(20)
+    H = np.conj(np.fft.fft(s, N))
+    y = ref.dmx_pulse_compression(x, 0, N, H)[0]
+    direct = np.array([sum(x[0, (n + k) % N] * np.conj(s[k]) for k in range(20)) for n in range(N)])
+    np.testing.assert_allclose(y, direct, rtol=0, atol=1e-10)
+
+
+@pytest.mark.parametrize("name,P,R", [("v2", 64, 1024), ("dmx", 64, 1024), ("legacy", 48, 1031), ("v2", 32, 2048)])
+def test_c_oracle_matches_numpy_oracle(name, P, R):
+    rng = np.random.default_rng(7)
+    echo = rng.standard_normal((2, P, R)) + 1j * rng.standard_normal((2, P, R))
+    echo[:, :, :R // 8] += 30.0
+    pre = coracle.preset(name, P, R)
+    rc = coracle.pc_mtd(echo, pre)
+    if name == "v2":
+        rn = np.stack([ref.fun_MTD_produce_v2(x, ref.v2_params(P, R)) for x in echo])
+    elif name == "dmx":
+        rn = np.stack([ref.fun_MTD_produce_dmx_syn(x, np.load(DATA + "/refDDCDataMF1.npy")) for x in echo])
+    else:
+        rn = np.stack([ref.fun_MTD_produce_legacy(x, np.load(DATA + "/legacy_pulse2.npy"),
+                                                  np.load(DATA + "/legacy_pulse3.npy")) for x in echo])
+    assert np.linalg.norm(rc - rn) / np.linalg.norm(rn) < 1e-13
+    M0 = ref.mtd_zero_num(P, pre["radar"]["wavelength"], pre["radar"]["prf"])
+    c = dict(refR=5, saveR=7, TR=4, methodR=0, refV=5, saveV=7, TV=4, methodV=0, M0=M0, rFlag=1, zero_v_div=20)
+    fc, fvc = coracle.cfar(rn, c, pre["cfar_segments"])
+    segs1 = [(a + 1, b) for a, b in pre["cfar_segments"]]
+    for i in range(rn.shape[0]):
+        f, fv = ref.main_cfar_chain(rn[i], c, segs1, 20)
+        np.testing.assert_array_equal(fc[i], f)
+        np.testing.assert_array_equal(fvc[i], fv)
+    assert fc.sum() > 0
