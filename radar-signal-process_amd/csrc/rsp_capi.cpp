@@ -4,7 +4,7 @@
 //
 // Chunking: the pulse-compression output of `chunk` CPIs is written to a scratch buffer
 // that is read back by the MTD kernel right after; chunk * P * R_out * 8 bytes is sized
-// (default 32 MiB) to stay in the 256 MiB Infinity Cache, so the corner turn between
+// (default 64 MiB) to stay in the 256 MiB Infinity Cache, so the corner turn between
 // the fast-time (PC) and slow-time (MTD) passes is served on-die instead of from HBM.
 #include <hip/hip_runtime.h>
 
@@ -33,6 +33,8 @@ struct rsp_ctx {
     std::string err;
     hipStream_t stream = nullptr;
     rsp::PcArgs pc{};
+    bool pc_v2 = false;                 // per-segment specialised kernels (pc_mf_kernel)
+    std::vector<rsp::PcMfArgs> pc_mf;   // one launch per matched-filter segment
     rsp::MtdArgs mtd{};
     size_t pc_lds = 0;
     int64_t chunk = 0;  // 0 = default
@@ -274,7 +276,12 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
             if (g.out_len != g.in_len)
                 return bail(fail(ctx, RSP_ERR_ARG, "segment %d: FIR needs out_len == in_len", s));
             d.ntaps = (int)g.coef_len;
-            for (int k = 0; k < d.ntaps; ++k) d.taps[k] = (float)g.coef_re[k];
+            std::vector<float> tf((size_t)d.ntaps);
+            for (int k = 0; k < d.ntaps; ++k) d.taps[k] = tf[k] = (float)g.coef_re[k];
+            float* dt = nullptr;
+            int rc = upload(ctx, tf, &dt);
+            if (rc) return bail(rc);
+            d.taps_dev = dt;
             int64_t sh = g.fir_shift % g.out_len;
             if (sh < 0) sh += g.out_len;
             d.fir_shift = (int)sh;
@@ -321,6 +328,41 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
         c = e;
     }
     ctx->pc_lds = rsp::pc_lds_bytes(max_nfft);
+    // Specialised path: at most one FIR segment, every MF length built, FIR staged in a slot
+    {
+        int nfir = 0, nmf = 0, fir_idx = -1;
+        bool ok = true;
+        for (int s = 0; s < p.nseg; ++s) {
+            if (pc.seg[s].kind == RSP_SEG_FIR) { ++nfir; fir_idx = s; }
+            else ++nmf;
+        }
+        ok = nfir <= 1 && nmf >= 1;
+        int first = 1;
+        for (int s = 0; s < p.nseg && ok; ++s) {
+            if (pc.seg[s].kind != RSP_SEG_MF) continue;
+            rsp::PcMfArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.R = (int)p.R;
+            a.R_out = (int)p.R_out;
+            a.mf = pc.seg[s];
+            if (first) {
+                a.do_fir = fir_idx >= 0;
+                if (a.do_fir) a.fir = pc.seg[fir_idx];
+                a.nzero = pc.nzero;
+                for (int z = 0; z < pc.nzero; ++z) {
+                    a.zero_lo[z] = pc.zero_lo[z];
+                    a.zero_hi[z] = pc.zero_hi[z];
+                }
+                if (!rsp::pc_mf_supported(a.mf.nfft, a.do_fir ? a.fir.in_len : 0)) ok = false;
+                first = 0;
+            } else if (!rsp::pc_mf_supported(a.mf.nfft, 0)) {
+                ok = false;
+            }
+            ctx->pc_mf.push_back(a);
+        }
+        ctx->pc_v2 = ok;
+        if (!ok) ctx->pc_mf.clear();
+    }
 
     // ---- MTD
     rsp::MtdArgs& m = ctx->mtd;
@@ -352,7 +394,7 @@ static int64_t chunk_of(const rsp_ctx* ctx, int64_t batch) {
     int64_t c = ctx->chunk;
     if (c <= 0) {
         const int64_t per = ctx->p.P * ctx->p.R_out * 8;
-        c = (32ll << 20) / (per > 0 ? per : 1);
+        c = (64ll << 20) / (per > 0 ? per : 1);
         if (c < 1) c = 1;
     }
     if (c > batch) c = batch;
@@ -432,6 +474,8 @@ static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_
 
 static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess; }
 
+static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s);
+
 // Run one kernel launch, bracketed by HIP events on `s` when profiling is on.
 template <typename F>
 static hipError_t timed(rsp_ctx* ctx, int k, hipStream_t s, F&& launch) {
@@ -450,6 +494,23 @@ static hipError_t timed(rsp_ctx* ctx, int k, hipStream_t s, F&& launch) {
     r = launch();
     if (r != hipSuccess) return r;
     return hipEventRecord(e.b, s);
+}
+
+static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s) {
+    if (!ctx->pc_v2)
+        return timed(ctx, RSP_K_PC, s, [&] { return rsp::launch_pc(ein, dtype, out, rows, ctx->pc, ctx->pc_lds, s); });
+    if (ctx->pc_mf.size() == 2 && rsp::pc_pair_supported(ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft)) {
+        rsp::PcMfArgs a1 = ctx->pc_mf[0], a2 = ctx->pc_mf[1];
+        a1.rows = a2.rows = (int)rows;
+        return timed(ctx, RSP_K_PC, s, [&] { return rsp::launch_pc_mf(ein, dtype, out, a1, &a2, s); });
+    }
+    for (const rsp::PcMfArgs& a0 : ctx->pc_mf) {
+        rsp::PcMfArgs a = a0;
+        a.rows = (int)rows;
+        hipError_t e = timed(ctx, RSP_K_PC, s, [&] { return rsp::launch_pc_mf(ein, dtype, out, a, nullptr, s); });
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 int rsp_profile(rsp_ctx* ctx, int32_t enable) {
@@ -485,8 +546,7 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
     if (!ctx || !d_echo || !d_pc || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: bad argument");
     if (dtype != RSP_C64 && dtype != RSP_C32F16) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: dtype %d", dtype);
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
-    HIP_TRY(ctx, rsp::launch_pc(d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, ctx->pc, ctx->pc_lds,
-                                (hipStream_t)stream));
+    HIP_TRY(ctx, run_pc(ctx, d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, (hipStream_t)stream));
     return RSP_OK;
 }
 
@@ -530,7 +590,7 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
         uint8_t* fv = nullptr;
         if (cfar) fv = d_flagV ? d_flagV + (size_t)c0 * P * Ro : (uint8_t*)ctx->tmp_flagV.p;
         float2* pcs = (float2*)ctx->scratch_pc.p;
-        HIP_TRY(ctx, timed(ctx, RSP_K_PC, s, [&] { return rsp::launch_pc(ein, dtype, pcs, n * P, ctx->pc, ctx->pc_lds, s); }));
+        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * P, s));
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, s, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, s); }));
         if (cfar) {
             uint8_t* fl = d_flag + (size_t)c0 * P * Ro;

@@ -192,4 +192,113 @@ __device__ __forceinline__ void fft_lds(float2* buf, int t, const float2* __rest
     fft_rec<N, G, 1>(buf, t, tw);
 }
 
+// ---------------------------------------------------------------- register-resident FFT
+// G threads share one length-N transform; thread t holds E = N/G elements in the
+// "strided" pattern u[m] = x[t + G*m].  Every Stockham pass with radix R | E gives each
+// thread PER = E/R butterflies j = t + i*G whose inputs are x[j + r*N/R] = u[i + r*PER],
+// so the first pass reads straight from registers (no LDS) and the last pass leaves
+// X[t + G*m] in u[m] -- natural order, coalesced for global stores, and exactly the input
+// pattern of the next transform (forward FFT -> spectrum multiply -> inverse FFT never
+// touches LDS in between).  Intermediate passes exchange through `buf` (N padded slots).
+__host__ __device__ constexpr int pick_radix_e(int rem, int e) {
+    if (rem % 16 == 0 && e % 16 == 0) return 16;
+    if (rem % 8 == 0 && e % 8 == 0) return 8;
+    if (rem % 4 == 0 && e % 4 == 0) return 4;
+    if (rem % 2 == 0 && e % 2 == 0) return 2;
+    if (rem % 3 == 0 && e % 3 == 0) return 3;
+    return 0;
+}
+
+// LDS slot of element (base + r*S) for r < R: affine in r whenever the padding allows it
+// (S a multiple of 16, or S == 1 with R | 16 and R | base), so the compiler emits one
+// address register and immediate offsets instead of R live addresses.
+template <int S, int R>
+__device__ __forceinline__ int slot(int base, int r) {
+    if constexpr (S % 16 == 0) return pidx(base) + r * (S + S / 16);
+    else if constexpr (S == 1 && 16 % R == 0) return pidx(base) + r;   // base is a multiple of R
+    else return pidx(base + r * S);
+}
+
+// v[r] *= W^(r*e) for r = 1..R-1, W = e^{-2 pi i/N}, from the fp32 table tw[0..N).
+// Radix 16 reads 6 table entries (W^e, W^2e, W^3e, W^4e, W^8e, W^12e) and forms the rest
+// with one complex product each (~1.5 ulp), instead of 15 gathers.
+template <int R, int N>
+__device__ __forceinline__ void twiddle(float2* v, int e, const float2* __restrict__ tw) {
+    if constexpr (R == 16) {
+        const float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+        const float2 w4 = tw[4 * e], w8 = tw[8 * e], w12 = tw[12 * e];
+        v[1] = cmul(v[1], w1);
+        v[2] = cmul(v[2], w2);
+        v[3] = cmul(v[3], w3);
+        v[4] = cmul(v[4], w4);
+        v[5] = cmul(v[5], cmul(w4, w1));
+        v[6] = cmul(v[6], cmul(w4, w2));
+        v[7] = cmul(v[7], cmul(w4, w3));
+        v[8] = cmul(v[8], w8);
+        v[9] = cmul(v[9], cmul(w8, w1));
+        v[10] = cmul(v[10], cmul(w8, w2));
+        v[11] = cmul(v[11], cmul(w8, w3));
+        v[12] = cmul(v[12], w12);
+        v[13] = cmul(v[13], cmul(w12, w1));
+        v[14] = cmul(v[14], cmul(w12, w2));
+        v[15] = cmul(v[15], cmul(w12, w3));
+    } else if constexpr (R == 8) {
+        const float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e], w4 = tw[4 * e];
+        v[1] = cmul(v[1], w1);
+        v[2] = cmul(v[2], w2);
+        v[3] = cmul(v[3], w3);
+        v[4] = cmul(v[4], w4);
+        v[5] = cmul(v[5], cmul(w4, w1));
+        v[6] = cmul(v[6], cmul(w4, w2));
+        v[7] = cmul(v[7], cmul(w4, w3));
+    } else {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * e]);
+    }
+}
+
+template <int N, int G, int Ns, int E>
+__device__ __forceinline__ void fft_reg(float2 (&u)[E], float2* buf, int t, const float2* __restrict__ tw) {
+    if constexpr (Ns < N) {
+        constexpr int R = pick_radix_e(N / Ns, E);
+        static_assert(R != 0, "no radix divides both the remaining length and E");
+        constexpr int NB = N / R;
+        constexpr int PER = E / R;
+        static_assert(NB == PER * G, "thread count and radix plan disagree");
+        if constexpr (Ns > 1) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int b = t + i * G;
+#pragma unroll
+                for (int r = 0; r < R; ++r) u[i + r * PER] = buf[slot<NB, R>(b, r)];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            float2 v[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = u[i + r * PER];
+            if constexpr (Ns > 1) {
+                const int k = (t + i * G) % Ns;
+                twiddle<R, N>(v, k * (N / (Ns * R)), tw);
+            }
+            dft<R>(v);
+#pragma unroll
+            for (int r = 0; r < R; ++r) u[i + r * PER] = v[r];
+        }
+        if constexpr (Ns * R < N) {
+            __syncthreads();  // WAR: earlier readers of buf are done
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int j = t + i * G;
+                const int base = (j / Ns) * Ns * R + (j % Ns);
+#pragma unroll
+                for (int r = 0; r < R; ++r) buf[slot<Ns, R>(base, r)] = u[i + r * PER];
+            }
+            __syncthreads();  // RAW
+        }
+        fft_reg<N, G, Ns * R, E>(u, buf, t, tw);
+    }
+}
+
 }  // namespace rsp

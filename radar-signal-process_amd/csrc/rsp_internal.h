@@ -21,6 +21,7 @@ struct SegDev {
     float scale;
     const float2* H;   // MF: conj(FFT_nfft(scale*replica)) / nfft
     const float2* tw;  // MF: W_nfft^e table, e < nfft
+    const float* taps_dev;  // FIR taps in device memory (no dynamic kernarg indexing)
     float taps[RSP_MAX_FIR_TAPS];
 };
 
@@ -31,6 +32,19 @@ struct PcArgs {
     int zero_lo[RSP_MAX_SEG + 1];
     int zero_hi[RSP_MAX_SEG + 1];
     SegDev seg[RSP_MAX_SEG];
+};
+
+// One matched-filter segment for every row, specialised on its FFT length; the first
+// launch of a chunk also runs the FIR segment and zero-fills uncovered columns.
+struct PcMfArgs {
+    int R, R_out;
+    int rows;
+    int do_fir;
+    SegDev fir;
+    SegDev mf;
+    int nzero;
+    int zero_lo[RSP_MAX_SEG + 1];
+    int zero_hi[RSP_MAX_SEG + 1];
 };
 
 // Doppler-dimension CFAR on one column tile (Function_CFAR1D_sub on used.').
@@ -71,6 +85,11 @@ size_t pc_lds_bytes(int max_nfft);
 
 hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, const PcArgs& a,
                      size_t lds_bytes, hipStream_t s);
+bool pc_mf_supported(int nfft, int fir_in_len);
+bool pc_pair_supported(int nfft1, int nfft2);
+// a2 == nullptr: one segment; otherwise both segments (a1.mf.nfft, a2->mf.nfft) in one launch
+hipError_t launch_pc_mf(const void* echo, int dtype, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
+                        hipStream_t s);
 hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
                       hipStream_t s);
 // Doppler CFAR straight from an RDM ([ncpi][V][R] fp32) for rsp_cfar.

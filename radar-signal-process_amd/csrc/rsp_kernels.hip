@@ -141,6 +141,186 @@ hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, con
     return hipGetLastError();
 }
 
+// ================================================================== pulse compression v2
+// One launch per matched-filter segment, specialised on its FFT length N: G threads per
+// PRT row (E = N/G elements each, register-resident Stockham passes), RPB rows per
+// 256..512-thread workgroup.  Row loads and stores are lane-contiguous (the strided
+// element pattern of fft_reg), the spectrum multiply sits between the forward and the
+// inverse FFT in registers, and the only LDS traffic is the inter-pass exchange.
+template <int N>
+struct PcCfg {
+    static constexpr int G = N / 16;                            // threads per row
+    static constexpr int E = N / G;                             // 16 elements per thread
+    static constexpr int RPB = G >= 256 ? 1 : 256 / G;          // rows per workgroup
+    static constexpr int T = G * RPB;
+    static constexpr int SLOT = padded_len(N);
+    static constexpr size_t lds = (size_t)RPB * SLOT * sizeof(float2);
+};
+
+template <typename TIn, int G>
+__device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
+                                        const SegDev& g, float* stage, bool valid, int t) {
+    // stage the segment's input, then y[n] = scale * sum_k taps[k] x[m-k], m = (n+shift) mod len
+    float2* s2 = reinterpret_cast<float2*>(stage);
+    for (int i = t; i < g.in_len; i += G) s2[i] = valid ? ld_c(x + g.in_start + i) : make_float2(0.f, 0.f);
+    __syncthreads();
+    for (int n = t; n < g.out_len; n += G) {
+        int m = n + g.fir_shift;
+        if (m >= g.out_len) m -= g.out_len;
+        float ar = 0.f, ai = 0.f;
+        const int kmax = m + 1 < g.ntaps ? m + 1 : g.ntaps;
+        const float* __restrict__ taps = g.taps_dev;
+        for (int k = 0; k < kmax; ++k) {
+            const float2 v = s2[m - k];
+            const float b = taps[k];
+            ar = fmaf(b, v.x, ar);
+            ai = fmaf(b, v.y, ai);
+        }
+        if (valid) y[g.out_start + n] = make_float2(ar * g.scale, ai * g.scale);
+    }
+    __syncthreads();
+}
+
+// One row's matched-filter segment (and optionally its FIR segment) by G threads.
+template <typename TIn, int N, int G>
+__device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
+                                       const PcMfArgs& a, int row, int t, float2* buf) {
+    constexpr int E = N / G;
+    const bool valid = row < a.rows;
+    const TIn* x = echo + (size_t)row * a.R;
+    float2* y = out + (size_t)row * a.R_out;
+    if (a.do_fir) {
+        if (valid)
+            for (int z = 0; z < a.nzero; ++z)
+                for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) y[c] = make_float2(0.f, 0.f);
+        fir_row<TIn, G>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
+    }
+    const int in_start = a.mf.in_start, in_len = a.mf.in_len;
+    const int out_start = a.mf.out_start, out_len = a.mf.out_len;
+    const float2* __restrict__ H = a.mf.H;
+    const float2* __restrict__ tw = a.mf.tw;
+    float2 u[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int i = t + G * m;
+        u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
+    }
+    fft_reg<N, G, 1, E>(u, buf, t, tw);
+#pragma unroll
+    for (int m = 0; m < E; ++m) u[m] = cconj(cmul(u[m], H[t + G * m]));  // conj(X.*H), 1/N in H
+    fft_reg<N, G, 1, E>(u, buf, t, tw);
+    if (valid) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int i = t + G * m;
+            if (i < out_len) y[out_start + i] = cconj(u[m]);
+        }
+    }
+}
+
+// Workgroup size shared by a pair of segment lengths: both run T threads (RPB = T/G rows).
+template <int N1, int N2>
+struct PairCfg {
+    static constexpr int T0 = PcCfg<N1>::G > PcCfg<N2>::G ? PcCfg<N1>::G : PcCfg<N2>::G;
+    static constexpr int T = T0 < 256 ? 256 : T0;
+    static constexpr int RPB1 = T / PcCfg<N1>::G, RPB2 = T / PcCfg<N2>::G;
+    static constexpr size_t L1 = (size_t)RPB1 * PcCfg<N1>::SLOT * sizeof(float2);
+    static constexpr size_t L2 = (size_t)RPB2 * PcCfg<N2>::SLOT * sizeof(float2);
+    static constexpr size_t lds = L1 > L2 ? L1 : L2;
+};
+
+// Single segment (N2 == 0) or two independent segments in one launch: blocks
+// [0, nblk2) run segment 2 (the long one, first for a short tail), the rest segment 1.
+template <typename TIn, int N1, int N2>
+__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 4) void pc_mf_kernel(
+    const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
+    constexpr int M2 = N2 ? N2 : N1;
+    using PC = PairCfg<N1, M2>;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if constexpr (N2 != 0) {
+        if ((int)blockIdx.x < nblk2) {
+            constexpr int G = PcCfg<N2>::G;
+            const int grp = threadIdx.x / G, t = threadIdx.x % G;
+            pc_row<TIn, N2, G>(echo, out, a2, blockIdx.x * PC::RPB2 + grp, t, lds + grp * PcCfg<N2>::SLOT);
+            return;
+        }
+    }
+    constexpr int G = PcCfg<N1>::G;
+    const int grp = threadIdx.x / G, t = threadIdx.x % G;
+    const int b = (int)blockIdx.x - (N2 ? nblk2 : 0);
+    pc_row<TIn, N1, G>(echo, out, a1, b * PC::RPB1 + grp, t, lds + grp * PcCfg<N1>::SLOT);
+}
+
+bool pc_mf_supported(int nfft, int fir_in_len) {
+    switch (nfft) {
+        case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: case 8192:
+        case 16384:
+            return fir_in_len <= padded_len(nfft);   // the FIR stages its input in the row's slot
+        default:
+            return false;
+    }
+}
+
+template <typename TIn, int N1, int N2>
+static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
+                                 hipStream_t s) {
+    constexpr int M2 = N2 ? N2 : N1;
+    using PC = PairCfg<N1, M2>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)pc_mf_kernel<TIn, N1, N2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)PC::lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int nblk1 = (a1.rows + PC::RPB1 - 1) / PC::RPB1;
+    const int nblk2 = N2 ? (a1.rows + PC::RPB2 - 1) / PC::RPB2 : 0;
+    dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
+    hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds, s, echo, out, a1,
+                       a2 ? *a2 : a1, nblk2);
+    return hipGetLastError();
+}
+
+#define RSP_PAIR(n1, n2) \
+    if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s)
+
+template <typename TIn>
+static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
+                                 hipStream_t s) {
+    // fused pairs of the built-in presets (v2 at 1024..16384 range bins, legacy)
+    RSP_PAIR(1024, 1024);
+    RSP_PAIR(1024, 4096);
+    RSP_PAIR(1024, 8192);
+    RSP_PAIR(1024, 16384);
+    RSP_PAIR(512, 1024);
+    if (a2) return hipErrorNotSupported;
+    switch (a1.mf.nfft) {
+        case 64: return launch_pc_mf_n<TIn, 64, 0>(echo, out, a1, nullptr, s);
+        case 128: return launch_pc_mf_n<TIn, 128, 0>(echo, out, a1, nullptr, s);
+        case 256: return launch_pc_mf_n<TIn, 256, 0>(echo, out, a1, nullptr, s);
+        case 512: return launch_pc_mf_n<TIn, 512, 0>(echo, out, a1, nullptr, s);
+        case 1024: return launch_pc_mf_n<TIn, 1024, 0>(echo, out, a1, nullptr, s);
+        case 2048: return launch_pc_mf_n<TIn, 2048, 0>(echo, out, a1, nullptr, s);
+        case 4096: return launch_pc_mf_n<TIn, 4096, 0>(echo, out, a1, nullptr, s);
+        case 8192: return launch_pc_mf_n<TIn, 8192, 0>(echo, out, a1, nullptr, s);
+        case 16384: return launch_pc_mf_n<TIn, 16384, 0>(echo, out, a1, nullptr, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+#undef RSP_PAIR
+
+bool pc_pair_supported(int n1, int n2) {
+    return (n1 == 1024 && (n2 == 1024 || n2 == 4096 || n2 == 8192 || n2 == 16384)) || (n1 == 512 && n2 == 1024);
+}
+
+hipError_t launch_pc_mf(const void* echo, int dtype, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
+                        hipStream_t s) {
+    if (a1.rows <= 0) return hipSuccess;
+    if (dtype == RSP_C64) return launch_pc_mf_t((const float2*)echo, out, a1, a2, s);
+    if (dtype == RSP_C32F16) return launch_pc_mf_t((const __half2*)echo, out, a1, a2, s);
+    return hipErrorInvalidValue;
+}
+
 // ================================================================== Doppler CFAR (column tile)
 // mag: W columns of V floats, column stride ms; flags written to out[v*R + r0 + c].
 __device__ __forceinline__ void doppler_cfar_tile(const float* mag, int ms, int V, int W,

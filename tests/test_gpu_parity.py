@@ -57,7 +57,7 @@ def test_pc_parity(torch_cuda, name, P, R):
         else:
             from rsp import presets
             H = ref.dmx_matched_filter(presets.load_data("refDDCDataMF1"), R)
-            want = ref.dmx_pulse_compression(e64[b:b + 1], 0, R, H)[0]
+            want = ref.dmx_pulse_compression(e64[b], 0, R, H)
         err = np.linalg.norm(got[b] - want) / np.linalg.norm(want)
         assert err < RDM_TOL, (name, b, err)
 
