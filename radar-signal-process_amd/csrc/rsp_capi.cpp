@@ -433,6 +433,8 @@ static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_
                 if (slo[s] < shi[q] && slo[q] < shi[s]) return fail(ctx, RSP_ERR_ARG, "CFAR: segments overlap");
         }
     }
+    if (cf->rFlag && cf->saveR + cf->refR + 2 > 32)
+        return fail(ctx, RSP_ERR_UNSUPPORTED, "CFAR: range guard+ref = %d > 30 not built", cf->saveR + cf->refR);
     if (cf->rFlag)
         for (int s = 0; s < nseg; ++s)
             if (shi[s] - slo[s] < 2 * (cf->saveR + cf->refR))
@@ -449,6 +451,7 @@ static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_
     cv->save = cf->saveV;
     cv->method = cf->methodV;
     cv->T = (float)cf->TV;
+    cv->Tr = (float)(cf->TV / cf->refV);
     cv->cz_lo = cz_lo;
     cv->cz_hi = cz_hi;
     cv->nseg = nseg;
@@ -462,6 +465,7 @@ static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_
     cr->save = cf->saveR;
     cr->method = cf->methodR;
     cr->T = (float)cf->TR;
+    cr->Tr = (float)(cf->TR / cf->refR);
     cr->cz_lo = cz_lo;
     cr->cz_hi = cz_hi;
     cr->nseg = nseg;

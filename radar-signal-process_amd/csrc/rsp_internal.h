@@ -53,6 +53,7 @@ struct CfarVArgs {
     int lo, hi;          // used rows [lo, hi) = rows M0+2 .. V-M0 (1-based)
     int ref, save, method;
     float T;
+    float Tr;            // T / ref (threshold = max|min(window sums) * Tr)
     int cz_lo, cz_hi;    // rows zeroed before CFAR (main_cfar.m:90-91), empty if lo >= hi
     int nseg;            // column segments (fun_CFARflag); columns outside get flag 0
     int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
@@ -74,6 +75,7 @@ struct CfarRArgs {
     int rflag;
     int ref, save, method;
     float T;
+    float Tr;            // T / ref
     int cz_lo, cz_hi;    // rows zeroed before CFAR
     int nseg;
     int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];

@@ -321,51 +321,83 @@ hipError_t launch_pc_mf(const void* echo, int dtype, float2* out, const PcMfArgs
     return hipErrorInvalidValue;
 }
 
-// ================================================================== Doppler CFAR (column tile)
-// mag: W columns of V floats, column stride ms; flags written to out[v*R + r0 + c].
-__device__ __forceinline__ void doppler_cfar_tile(const float* mag, int ms, int V, int W,
-                                                  const CfarVArgs& cv, uint8_t* __restrict__ out,
-                                                  int r0, int R, int t) {
-    for (int e = t; e < V * W; e += kBlock) {
-        const int c = e % W, v = e / W, r = r0 + c;
-        if (r >= R) continue;
-        bool in_seg = false;
-        for (int s = 0; s < cv.nseg; ++s) in_seg |= (r >= cv.seg_lo[s] && r < cv.seg_hi[s]);
-        uint8_t f = 0;
-        if (in_seg && v >= cv.lo && v < cv.hi) {
-            const float* col = mag + c * ms;
-            const int l1 = v - cv.save - cv.ref;  // left window [l1, v-save-1]
-            const int r1 = v + cv.save + 1;       // right window [r1, v+save+ref]
-            const bool lok = l1 >= cv.lo;
-            const bool rok = r1 + cv.ref - 1 < cv.hi;
-            float sl = 0.f, sr = 0.f;
-            if (lok)
-                for (int i = 0; i < cv.ref; ++i) sl += col[l1 + i];
-            if (rok)
-                for (int i = 0; i < cv.ref; ++i) sr += col[r1 + i];
-            const float lavg = (lok ? sl : sr) / (float)cv.ref;   // mean() of 5 cells
-            const float ravg = (rok ? sr : sl) / (float)cv.ref;
-            const float avg = cv.method == 0 ? fmaxf(lavg, ravg) : fminf(lavg, ravg);
-            f = col[v] >= avg * cv.T ? 1 : 0;
+// ================================================================== CFAR building blocks
+// Reference windows of Function_CFAR1D_sub.m:25-28 around cell y of a line whose valid
+// part is [lo, hi): left = [y-save-ref, y-save-1], right = [y+save+1, y+save+ref]; a side
+// that leaves [lo, hi) is replaced by the other side's mean (:30-39).  Window sums are
+// precomputed as direct left-to-right sums of `ref` cells (the order mean() adds them),
+// so a cell needs two sum lookups.  max/min of the two means = max/min of the two sums
+// divided once (division by a positive constant is monotonic in IEEE arithmetic).
+__device__ __forceinline__ uint8_t cfar_test(float x, float sl, float sr, bool lok, bool rok, int method, float Tr) {
+    // fp32 threshold max|min(sum_L, sum_R) * (T/ref); the fp64 reference computes
+    // (sum/ref)*T -- the two differ by ~1 ulp, far inside the near-threshold band
+    const float a = lok ? sl : sr;
+    const float b = rok ? sr : sl;
+    return x >= (method == 0 ? fmaxf(a, b) : fminf(a, b)) * Tr ? 1 : 0;
+}
+
+__device__ __forceinline__ bool in_segs(int c, int nseg, const int* lo, const int* hi) {
+    bool in = false;
+#pragma unroll
+    for (int s = 0; s < RSP_MAX_SEG; ++s)
+        if (s < nseg) in |= (c >= lo[s] && c < hi[s]);
+    return in;
+}
+
+__device__ __forceinline__ void seg_of(int c, int nseg, const int* lo, const int* hi, int& slo, int& shi) {
+    slo = 0;
+    shi = 0;
+#pragma unroll
+    for (int s = 0; s < RSP_MAX_SEG; ++s)
+        if (s < nseg && c >= lo[s] && c < hi[s]) {
+            slo = lo[s];
+            shi = hi[s];
         }
-        out[(size_t)v * R + r] = f;
+}
+
+// Doppler CFAR over a column-major tile in LDS: column c = mag[c*ms + v], v < V (zero band
+// already applied).  Thread (c, g) owns rows [v0, v1); sums[c*ms + a] must hold the window
+// sums for every a with a + ref <= V.  Writes flags to out[v*R] (out already offset by r).
+__device__ __forceinline__ void doppler_sums(const float* mag, float* sums, int V, int ref, int v0, int v1) {
+    for (int a = v0; a < v1; ++a) {
+        if (a + ref > V) break;
+        float s = 0.f;
+        for (int k = 0; k < ref; ++k) s += mag[a + k];
+        sums[a] = s;
+    }
+}
+
+__device__ __forceinline__ void doppler_flags(const float* mag, const float* sums, const CfarVArgs& cv, bool col_on,
+                                              int v0, int v1, uint8_t* __restrict__ out, size_t R, bool rv) {
+    out += (size_t)v0 * R;
+    for (int v = v0; v < v1; ++v) {
+        uint8_t f = 0;
+        if (col_on && v >= cv.lo && v < cv.hi) {
+            const int l1 = v - cv.save - cv.ref, r1 = v + cv.save + 1;
+            const bool lok = l1 >= cv.lo, rok = r1 + cv.ref <= cv.hi;
+            f = cfar_test(mag[v], lok ? sums[l1] : 0.f, rok ? sums[r1] : 0.f, lok, rok, cv.method, cv.Tr);
+        }
+        if (rv) *out = f;
+        out += R;
     }
 }
 
 // ================================================================== MTD (+ Doppler CFAR)
-__host__ __device__ constexpr int pow2floor(int x) {
-    int p = 1;
-    while (p * 2 <= x) p *= 2;
-    return p;
-}
-
+// One workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the tile,
+// pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
+// samples load straight into registers with W-wide coalesced rows, the slow-time FFT
+// runs register-resident with LDS exchanges, and |X| leaves in coalesced RDM rows.
 template <int P>
 struct MtdCfg {
-    static constexpr int G = (P / 16) < 1 ? 1 : ((P / 16) >= 64 ? 64 : pow2floor(P / 16));
-    static constexpr int W = kBlock / G;           // range bins per workgroup
-    static constexpr int CS = padded_len(P);       // float2 stride of one column
-    static constexpr int MS = P + 1;               // float stride of one magnitude column
-    static constexpr size_t lds = (size_t)W * CS * sizeof(float2) + (size_t)W * MS * sizeof(float);
+    static constexpr int E = (P % 3 == 0) ? 24 : 16;   // elements per thread
+    static constexpr int G = P / E;                    // threads per range bin
+    static constexpr int W = kBlock / G;               // range bins per workgroup
+    static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
+    static constexpr int MS = P + 1;                   // odd float stride of a CFAR column
+    static constexpr size_t lds_fft = (size_t)W * SLOT * sizeof(float2);
+    static constexpr size_t lds_cfar = (size_t)2 * W * MS * sizeof(float);
+    static constexpr size_t lds = lds_fft > lds_cfar ? lds_fft : lds_cfar;
+    static_assert(G * E == P && (G & (G - 1)) == 0 && G <= kBlock, "MTD tiling");
 };
 
 template <int P>
@@ -373,41 +405,53 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
     using C = MtdCfg<P>;
+    constexpr int G = C::G, E = C::E, W = C::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* cbuf = reinterpret_cast<float2*>(smem);
-    float* mag = reinterpret_cast<float*>(smem + (size_t)C::W * C::CS * sizeof(float2));
-    const int t = threadIdx.x;
+    const int c = threadIdx.x % W, g = threadIdx.x / W;
     const size_t cpi = blockIdx.y;
-    const int r0 = blockIdx.x * C::W;
     const int R = a.R_out;
-    const float2* src = pc + cpi * (size_t)P * R;
-
-    for (int e = t; e < P * C::W; e += kBlock) {
-        const int c = e % C::W, p = e / C::W, r = r0 + c;
-        float2 v = make_float2(0.f, 0.f);
-        if (r < R) v = src[(size_t)p * R + r];
+    const int r = blockIdx.x * W + c;
+    const bool rv = r < R;
+    const float2* src = pc + cpi * (size_t)P * R + (rv ? r : 0);
+    float2 u[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int p = g + G * m;
+        const float2 v = rv ? src[(size_t)p * R] : make_float2(0.f, 0.f);
         const float w = a.win[p];
-        cbuf[c * C::CS + pidx(p)] = make_float2(v.x * w, v.y * w);
+        u[m] = make_float2(v.x * w, v.y * w);
+    }
+    fft_reg<P, G, 1, E>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, a.tw);
+
+    float* dst = rdm + cpi * (size_t)P * R + r;
+    float mg[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int q = g + G * m;          // FFT bin
+        int v = q + a.shift;              // fftshift: out[v] = X[(v - shift) mod P]
+        if (v >= P) v -= P;
+        float mm = sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
+        if (v >= a.z_lo && v < a.z_hi) mm = 0.f;   // fun_0v_pressing
+        mg[m] = mm;
+        if (rv) dst[(size_t)v * R] = mm;
+    }
+    if (!a.cv.enabled) return;
+    __syncthreads();  // the FFT exchange slots are free from here on
+    float* mag = reinterpret_cast<float*>(smem) + c * C::MS;
+    float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::MS;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int q = g + G * m;
+        int v = q + a.shift;
+        if (v >= P) v -= P;
+        mag[v] = (v >= a.cv.cz_lo && v < a.cv.cz_hi) ? 0.f : mg[m];   // main_cfar.m:90-91
     }
     __syncthreads();
-    fft_lds<P, C::G>(cbuf + (t / C::G) * C::CS, t % C::G, a.tw);
-
-    float* dst = rdm + cpi * (size_t)P * R;
-    const bool cfar = a.cv.enabled != 0;
-    for (int e = t; e < P * C::W; e += kBlock) {
-        const int c = e % C::W, v = e / C::W, r = r0 + c;
-        int q = v - a.shift;
-        if (q < 0) q += P;
-        const float2 X = cbuf[c * C::CS + pidx(q)];
-        float m = sqrtf(fmaf(X.x, X.x, X.y * X.y));
-        if (v >= a.z_lo && v < a.z_hi) m = 0.f;
-        if (r < R) dst[(size_t)v * R + r] = m;
-        if (cfar) mag[c * C::MS + v] = (v >= a.cv.cz_lo && v < a.cv.cz_hi) ? 0.f : m;
-    }
-    if (cfar) {
-        __syncthreads();
-        doppler_cfar_tile(mag, C::MS, P, C::W, a.cv, flagV + cpi * (size_t)P * R, r0, R, t);
-    }
+    const int v0 = g * E, v1 = v0 + E;   // this thread's run of Doppler rows
+    doppler_sums(mag, sums, P, a.cv.ref, v0, v1);
+    __syncthreads();
+    const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
+    doppler_flags(mag, sums, a.cv, col_on, v0, v1, flagV + cpi * (size_t)P * R + r, R, rv);
 }
 
 template <int P>
@@ -458,31 +502,37 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
 }
 
 // ================================================================== Doppler CFAR from an RDM
+// rsp_cfar's first stage: tile of W columns x V rows staged column-major in LDS.
 __global__ __launch_bounds__(kBlock) void cfar_v_kernel(const float* __restrict__ rdm,
                                                         uint8_t* __restrict__ flagV, int V, int R,
-                                                        int W, CfarVArgs cv) {
+                                                        int lw, CfarVArgs cv) {
     extern __shared__ __attribute__((aligned(16))) float magv[];
-    const int t = threadIdx.x;
+    const int W = 1 << lw, G = kBlock >> lw;
+    const int c = threadIdx.x & (W - 1), g = threadIdx.x >> lw;
     const size_t cpi = blockIdx.y;
-    const int r0 = blockIdx.x * W;
+    const int r = blockIdx.x * W + c;
+    const bool rv = r < R;
     const int ms = V + 1;
-    const float* src = rdm + cpi * (size_t)V * R;
-    for (int e = t; e < V * W; e += kBlock) {
-        const int c = e % W, v = e / W, r = r0 + c;
-        float m = 0.f;
-        if (r < R && !(v >= cv.cz_lo && v < cv.cz_hi)) m = src[(size_t)v * R + r];
-        magv[c * ms + v] = m;
-    }
+    float* mag = magv + c * ms;
+    float* sums = magv + W * ms + c * ms;
+    const float* src = rdm + cpi * (size_t)V * R + (rv ? r : 0);
+    for (int v = g; v < V; v += G)
+        mag[v] = (rv && !(v >= cv.cz_lo && v < cv.cz_hi)) ? src[(size_t)v * R] : 0.f;
     __syncthreads();
-    doppler_cfar_tile(magv, ms, V, W, cv, flagV + cpi * (size_t)V * R, r0, R, t);
+    const int run = (V + G - 1) / G;
+    const int v0 = g * run, v1 = v0 + run < V ? v0 + run : V;
+    doppler_sums(mag, sums, V, cv.ref, v0, v1);
+    __syncthreads();
+    const bool col_on = rv && in_segs(r, cv.nseg, cv.seg_lo, cv.seg_hi);
+    doppler_flags(mag, sums, cv, col_on, v0, v1, flagV + cpi * (size_t)V * R + r, R, rv);
 }
 
 hipError_t launch_cfar_v(const float* rdm, uint8_t* flagV, int ncpi, int V, int R,
                          const CfarVArgs& a, hipStream_t s) {
     if (ncpi <= 0) return hipSuccess;
-    int W = 64;
-    while (W > 1 && (size_t)W * (V + 1) * sizeof(float) > 64 * 1024) W /= 2;
-    const size_t lds = (size_t)W * (V + 1) * sizeof(float);
+    int lw = 6;
+    while (lw > 0 && (size_t)2 * (1 << lw) * (V + 1) * sizeof(float) > 96 * 1024) --lw;
+    const size_t lds = (size_t)2 * (1 << lw) * (V + 1) * sizeof(float);
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)cfar_v_kernel,
@@ -490,13 +540,22 @@ hipError_t launch_cfar_v(const float* rdm, uint8_t* flagV, int ncpi, int V, int 
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    dim3 grid((unsigned)((R + W - 1) / W), (unsigned)ncpi), block(kBlock);
-    hipLaunchKernelGGL(cfar_v_kernel, grid, block, lds, s, rdm, flagV, V, R, W, a);
+    dim3 grid((unsigned)((R + (1 << lw) - 1) >> lw), (unsigned)ncpi), block(kBlock);
+    hipLaunchKernelGGL(cfar_v_kernel, grid, block, lds, s, rdm, flagV, V, R, lw, a);
     return hipGetLastError();
 }
 
 // ================================================================== range CFAR + re-localisation
-__global__ __launch_bounds__(kBlock) void cfar_r_kernel(const float* __restrict__ rdm,
+// One workgroup per RDM row.  Phase 1 stages the row (+ zero halo) and its Doppler flags in
+// LDS; phase 2 forms the range window sums; phase 3 evaluates the range CFAR at every cell
+// (Function_CFAR1D_sub_fixCells.m:34-58 -- the decision at a cell does not depend on which
+// hit asked for it); phase 4 resolves executeCFAR.m:45-84 as a gather: cell c is flagged iff
+// some Doppler hit r in {c-1, c, c+1} of c's segment picks c as the first maximum among its
+// passing cells {r-1, r, r+1}.  Each thread handles 4 adjacent cells per step, so flags
+// leave as coalesced 32-bit words.
+constexpr int kHalo = 32;   // >= guard + ref + 2 (checked on the host)
+
+__global__ __launch_bounds__(kBlock) void cfar_r_generic_kernel(const float* __restrict__ rdm,
                                                         const uint8_t* __restrict__ flagV,
                                                         uint8_t* __restrict__ flag, CfarRArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -515,73 +574,214 @@ __global__ __launch_bounds__(kBlock) void cfar_r_kernel(const float* __restrict_
         for (int c = t; c < R; c += kBlock) out[c] = fv_g[c];
         return;
     }
-    float* x = reinterpret_cast<float*>(smem);
-    uint8_t* fv = smem + (size_t)R * sizeof(float);
-    uint8_t* pass = fv + R;
+    const int Rp = (R + 3) & ~3;                      // row length rounded to words
+    const int L = Rp + 2 * kHalo;
+    float* xs = reinterpret_cast<float*>(smem) + kHalo;          // xs[-kHalo, Rp + kHalo)
+    float* ss = xs + L;                                            // window sums, same indexing
+    uint8_t* pass = reinterpret_cast<uint8_t*>(ss - kHalo + L) + kHalo;   // pass[-kHalo, Rp+kHalo)
+    uint8_t* fv = pass + L;                                        // fv[-kHalo, Rp+kHalo)
     const bool zrow = (v >= a.cz_lo && v < a.cz_hi);
     const float* xr = rdm + rowoff;
-    for (int c = t; c < R; c += kBlock) {
-        x[c] = zrow ? 0.f : xr[c];
-        fv[c] = fv_g[c];
+    for (int i = t; i < L; i += kBlock) {
+        const int c = i - kHalo;
+        const bool in = c >= 0 && c < R;
+        xs[c] = (in && !zrow) ? xr[c] : 0.f;
+        fv[c] = in ? fv_g[c] : 0;
+        pass[c] = 0;
+    }
+    __syncthreads();
+    const int ref = a.ref;
+    for (int i = t; i < L; i += kBlock) {
+        const int c = i - kHalo;
+        if (c + ref > Rp + kHalo) continue;
+        float s = 0.f;
+        for (int k = 0; k < ref; ++k) s += xs[c + k];
+        ss[c] = s;
     }
     __syncthreads();
     for (int c = t; c < R; c += kBlock) {
-        int slo = 0, shi = 0;
-        for (int s = 0; s < a.nseg; ++s)
-            if (c >= a.seg_lo[s] && c < a.seg_hi[s]) { slo = a.seg_lo[s]; shi = a.seg_hi[s]; }
+        int slo, shi;
+        seg_of(c, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
         uint8_t p = 0;
         if (shi > slo) {
-            const int l1 = c - a.save - a.ref;
-            const int r1 = c + a.save + 1;
-            const bool lok = l1 >= slo;
-            const bool rok = r1 + a.ref - 1 < shi;
-            float sl = 0.f, sr = 0.f;
-            if (lok)
-                for (int i = 0; i < a.ref; ++i) sl += x[l1 + i];
-            if (rok)
-                for (int i = 0; i < a.ref; ++i) sr += x[r1 + i];
-            const float lavg = (lok ? sl : sr) / (float)a.ref;
-            const float ravg = (rok ? sr : sl) / (float)a.ref;
-            const float avg = a.method == 0 ? fmaxf(lavg, ravg) : fminf(lavg, ravg);
-            p = x[c] >= avg * a.T ? 1 : 0;
+            const int l1 = c - a.save - ref, r1 = c + a.save + 1;
+            const bool lok = l1 >= slo, rok = r1 + ref <= shi;
+            p = cfar_test(xs[c], lok ? ss[l1] : 0.f, rok ? ss[r1] : 0.f, lok, rok, a.method, a.Tr);
         }
         pass[c] = p;
     }
     __syncthreads();
-    for (int c = t; c < R; c += kBlock) {
-        int slo = 0, shi = 0;
-        for (int s = 0; s < a.nseg; ++s)
-            if (c >= a.seg_lo[s] && c < a.seg_hi[s]) { slo = a.seg_lo[s]; shi = a.seg_hi[s]; }
-        uint8_t f = 0;
-        for (int d = -1; d <= 1 && shi > slo; ++d) {
-            const int r = c + d;  // a Doppler hit at r tests cells r-1..r+1
-            if (r < slo || r >= shi || !fv[r]) continue;
-            int best = -1;
-            float bx = 0.f;
-            for (int e2 = -1; e2 <= 1; ++e2) {
-                const int q = r + e2;
-                if (q < slo || q >= shi || !pass[q]) continue;
-                if (best < 0 || x[q] > bx) { best = q; bx = x[q]; }  // first max
+    for (int c0 = 4 * t; c0 < R; c0 += 4 * kBlock) {
+        // x, pass at c0-2 .. c0+5 and fv at c0-1 .. c0+4, from aligned words
+        float xw[12];
+        const float4 xa = *reinterpret_cast<const float4*>(xs + c0 - 4);
+        const float4 xb = *reinterpret_cast<const float4*>(xs + c0);
+        const float4 xc = *reinterpret_cast<const float4*>(xs + c0 + 4);
+        xw[0] = xa.x; xw[1] = xa.y; xw[2] = xa.z; xw[3] = xa.w;
+        xw[4] = xb.x; xw[5] = xb.y; xw[6] = xb.z; xw[7] = xb.w;
+        xw[8] = xc.x; xw[9] = xc.y; xw[10] = xc.z; xw[11] = xc.w;
+        const uint32_t pa = *reinterpret_cast<const uint32_t*>(pass + c0 - 4);
+        const uint32_t pb = *reinterpret_cast<const uint32_t*>(pass + c0);
+        const uint32_t pcw = *reinterpret_cast<const uint32_t*>(pass + c0 + 4);
+        const uint32_t fa = *reinterpret_cast<const uint32_t*>(fv + c0 - 4);
+        const uint32_t fb = *reinterpret_cast<const uint32_t*>(fv + c0);
+        const uint32_t fc = *reinterpret_cast<const uint32_t*>(fv + c0 + 4);
+        const uint64_t pw = (uint64_t)pa | ((uint64_t)pb << 32);   // byte k <-> cell c0-4+k
+        const uint64_t fw = (uint64_t)fa | ((uint64_t)fb << 32);
+        auto P_ = [&](int k) -> bool {   // pass at cell c0-4+k, k in [0, 12)
+            return k < 8 ? ((pw >> (8 * k)) & 0xff) != 0 : ((pcw >> (8 * (k - 8))) & 0xff) != 0;
+        };
+        auto F_ = [&](int k) -> bool {
+            return k < 8 ? ((fw >> (8 * k)) & 0xff) != 0 : ((fc >> (8 * (k - 8))) & 0xff) != 0;
+        };
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = c0 + j;
+            int slo, shi;
+            seg_of(c, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
+            bool f = false;
+#pragma unroll
+            for (int d = -1; d <= 1; ++d) {
+                const int rr = c + d;   // a Doppler hit at rr tests cells rr-1 .. rr+1
+                if (rr < slo || rr >= shi || !F_(4 + j + d)) continue;
+                int best = -100;
+                float bx = 0.f;
+#pragma unroll
+                for (int e = -1; e <= 1; ++e) {
+                    const int q = rr + e;
+                    const int k = 4 + j + d + e;
+                    if (q < slo || q >= shi || !P_(k)) continue;
+                    if (best == -100 || xw[k] > bx) { best = d + e; bx = xw[k]; }   // first max
+                }
+                f |= (best == 0);
             }
-            if (best == c) f = 1;
+            if (c < R && f) word |= 1u << (8 * j);
         }
-        out[c] = f;
+        if (c0 + 3 < R && (R & 3) == 0) {
+            *reinterpret_cast<uint32_t*>(out + c0) = word;
+        } else {
+            for (int j = 0; j < 4 && c0 + j < R; ++j) out[c0 + j] = (word >> (8 * j)) & 0xff;
+        }
     }
+}
+
+
+// Range CFAR specialised on the window (REF reference + SAVE guard cells; the reference
+// uses 5 + 7): no LDS and no barriers.  Thread = 4 adjacent cells c0..c0+3 of one row; it
+// reads x[c0-16, c0+20) as aligned float4s from L2 (neighbouring threads overlap in L1),
+// forms the 16 window sums it needs in MATLAB's summation order, evaluates the range test
+// at c0-2 .. c0+5 and resolves the four outputs as in cfar_r_generic_kernel.  Cells whose
+// windows cross a segment edge take the segment-aware branch.
+template <int REF, int SAVE>
+__global__ __launch_bounds__(kBlock) void cfar_r_kernel(const float* __restrict__ rdm,
+                                                        const uint8_t* __restrict__ flagV,
+                                                        uint8_t* __restrict__ flag, CfarRArgs a, int groups) {
+    constexpr int H = SAVE + REF + 2;          // farthest x offset a result depends on
+    constexpr int B = (H + 3) & ~3;            // aligned halo
+    constexpr int NX = 4 + 2 * B;              // x values held per thread
+    const int R = a.R;
+    const int v = blockIdx.x / groups;
+    const int c0 = ((blockIdx.x % groups) * kBlock + threadIdx.x) * 4;
+    if (c0 >= R) return;
+    const size_t cpi = blockIdx.y;
+    const size_t rowoff = (cpi * (size_t)a.V + v) * (size_t)R;
+    uint32_t* out = reinterpret_cast<uint32_t*>(flag + rowoff + c0);
+    if (v < a.lo || v >= a.hi) {
+        *out = 0u;
+        return;
+    }
+    const uint32_t* fvw = reinterpret_cast<const uint32_t*>(flagV + rowoff);
+    const uint32_t fa = c0 >= 4 ? fvw[c0 / 4 - 1] : 0u;
+    const uint32_t fb = fvw[c0 / 4];
+    const uint32_t fc = c0 + 4 < R ? fvw[c0 / 4 + 1] : 0u;
+    if ((fa >> 24) == 0 && fb == 0 && (fc & 0xff) == 0) {   // no Doppler hit can reach these cells
+        *out = 0u;
+        return;
+    }
+    const bool zrow = (v >= a.cz_lo && v < a.cz_hi);
+    const float* xr = rdm + rowoff;
+    float x[NX];   // x[k] = row[c0 - B + k]
+#pragma unroll
+    for (int k = 0; k < NX; k += 4) {
+        const int c = c0 - B + k;
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!zrow && c >= 0 && c + 3 < R) q = *reinterpret_cast<const float4*>(xr + c);
+        x[k] = q.x; x[k + 1] = q.y; x[k + 2] = q.z; x[k + 3] = q.w;
+    }
+    int slo, shi;
+    seg_of(c0, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
+    const bool simple = (c0 - H >= slo) && (c0 + 3 + H < shi);   // all windows inside one segment
+    bool pass[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {   // cell q = c0 - 2 + i, x index B - 2 + i
+        const int xi = B - 2 + i;
+        float sl = 0.f, sr = 0.f;
+#pragma unroll
+        for (int k = 0; k < REF; ++k) sl += x[xi - SAVE - REF + k];
+#pragma unroll
+        for (int k = 0; k < REF; ++k) sr += x[xi + SAVE + 1 + k];
+        if (simple) {
+            pass[i] = x[xi] >= (a.method == 0 ? fmaxf(sl, sr) : fminf(sl, sr)) * a.Tr;
+        } else {
+            const int q = c0 - 2 + i;
+            int ql, qh;
+            seg_of(q, a.nseg, a.seg_lo, a.seg_hi, ql, qh);
+            const bool lok = q - SAVE - REF >= ql, rok = q + SAVE + REF < qh;
+            pass[i] = (qh > ql) && cfar_test(x[xi], sl, sr, lok, rok, a.method, a.Tr);
+        }
+    }
+    const uint64_t fw = (uint64_t)fa | ((uint64_t)fb << 32);   // byte k <-> cell c0 - 4 + k
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        int cl = slo, ch = shi;
+        if (!simple) seg_of(c, a.nseg, a.seg_lo, a.seg_hi, cl, ch);
+        bool f = false;
+#pragma unroll
+        for (int d = -1; d <= 1; ++d) {
+            const int rr = c + d;
+            const int fk = 4 + j + d;
+            const bool hit = fk < 8 ? ((fw >> (8 * fk)) & 0xff) != 0 : ((fc >> (8 * (fk - 8))) & 0xff) != 0;
+            if (!hit || rr < cl || rr >= ch) continue;
+            int best = -100;
+            float bx = 0.f;
+#pragma unroll
+            for (int e = -1; e <= 1; ++e) {
+                const int q = rr + e;
+                const int i = 2 + j + d + e;   // pass/x index of cell q
+                if (q < cl || q >= ch || !pass[i]) continue;
+                const float xv = x[B - 2 + i];
+                if (best == -100 || xv > bx) { best = d + e; bx = xv; }   // first max
+            }
+            f |= (best == 0);
+        }
+        if (f) word |= 1u << (8 * j);
+    }
+    *out = word;
 }
 
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
                          const CfarRArgs& a, hipStream_t s) {
     if (ncpi <= 0) return hipSuccess;
-    const size_t lds = (size_t)a.R * (sizeof(float) + 2);
+    const int L = ((a.R + 3) & ~3) + 2 * kHalo;
+    const size_t lds = (size_t)L * (2 * sizeof(float) + 2);
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)cfar_r_kernel,
+        hipError_t e = hipFuncSetAttribute((const void*)cfar_r_generic_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
+    if (a.ref == 5 && a.save == 7 && a.rflag && (a.R & 3) == 0) {   // the reference's parameters
+        const int groups = (a.R / 4 + kBlock - 1) / kBlock;
+        dim3 grid((unsigned)(groups * a.V), (unsigned)ncpi), block(kBlock);
+        hipLaunchKernelGGL((cfar_r_kernel<5, 7>), grid, block, 0, s, rdm, flagV, flag, a, groups);
+        return hipGetLastError();
+    }
     dim3 grid((unsigned)a.V, (unsigned)ncpi), block(kBlock);
-    hipLaunchKernelGGL(cfar_r_kernel, grid, block, lds, s, rdm, flagV, flag, a);
+    hipLaunchKernelGGL(cfar_r_generic_kernel, grid, block, lds, s, rdm, flagV, flag, a);
     return hipGetLastError();
 }
 

@@ -19,3 +19,6 @@ if [ "${PROFILE:-1}" = "1" ]; then
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$ROOT/gpurun_out/prof.log"
   find "$ROOT/gpurun_out/prof" -name "*stats*" | head
 fi
+if [ "${PMC:-0}" = "1" ]; then
+  bash "$ROOT/tools/pmc.sh"
+fi

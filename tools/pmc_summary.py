@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (gpurun_out/pmc/g*/run_counter_collection.csv) per kernel.
+
+Prints the mean counter value per dispatch and derived figures.  gfx950 corrections
+(MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide coalesced read,
+so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B stores (KiB units).
+Usage: pmc_summary.py [pmc_dir] [--json out.json --cpis-per-dispatch N]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name):
+    for k in ("pc_mf_kernel", "pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "cfar_fused"):
+        if k in name:
+            return k
+    return name[:40]
+
+
+def load(pmc_dir):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "g*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] in ("FETCH_SIZE",):
+                dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return acc, dur
+
+
+def main():
+    args = sys.argv[1:]
+    pmc_dir = args[0] if args and not args[0].startswith("--") else "gpurun_out/pmc"
+    acc, dur = load(pmc_dir)
+    rows = {}
+    for k, cs in acc.items():
+        if not any(x in k for x in ("pc_", "mtd", "cfar")):
+            continue
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = sum(dur[k]) / len(dur[k]) if dur[k] else float("nan")
+        rd = 2 * m.get("FETCH_SIZE", 0) * 1024
+        wr = m.get("WRITE_SIZE", 0) * 1024
+        row = {"dispatches": len(cs.get("FETCH_SIZE", [])), "avg_us_profiled": round(d, 2),
+               "read_MB": round(rd / 1e6, 3), "write_MB": round(wr / 1e6, 3),
+               "GBps": round((rd + wr) / (d * 1e3), 1) if d == d and d > 0 else None}
+        for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                  "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS",
+                  "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                  "SQ_ACTIVE_INST_ANY", "TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE"):
+            if c in m:
+                row[c] = m[c]
+        if "TCC_HIT_sum" in m:
+            row["L2_hit"] = round(m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 3)
+        if "GRBM_GUI_ACTIVE" in m and d == d and d > 0:
+            row["eff_clock_GHz"] = round(m["GRBM_GUI_ACTIVE"] / 8 / (d * 1e3), 3)
+        if "SQ_WAVE_CYCLES" in m and "SQ_WAIT_ANY" in m:
+            wc = m["SQ_WAVE_CYCLES"]
+            row["wait_frac"] = round(m["SQ_WAIT_ANY"] / wc, 3)
+            row["valu_frac"] = round(m.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3)
+            row["lds_frac"] = round(m.get("SQ_ACTIVE_INST_LDS", 0) / wc, 3)
+        rows[k] = row
+    for k, r in rows.items():
+        print(k)
+        for c, v in r.items():
+            print("   %-22s %s" % (c, v))
+    if "--json" in args:
+        out = args[args.index("--json") + 1]
+        json.dump(rows, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
