@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-cfar", action="store_true", help="PC + MTD only (config c2)")
     ap.add_argument("--half", action="store_true", help="fp16 I/Q input (config c5 style)")
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
     return ap.parse_args()
@@ -102,7 +103,7 @@ def main():
 
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)
-    eng = Engine(spec, device=local, chunk=args.chunk)
+    eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
     B, P, R = args.batch, spec.P, spec.R_out
     # contiguous shard of the CPI stream per rank: seed = 1000 + config id 3 + first CPI index
     echo = synth.echo_torch(spec, B, seed=1003 + rank * B, device=dev, half=args.half)

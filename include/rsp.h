@@ -144,6 +144,11 @@ const char* rsp_last_error(const rsp_ctx* ctx);
  * stay in the 256 MiB Infinity Cache).  0 restores the default. */
 int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 
+/* Number of chunk pipelines (1..4, default 2): chunk k runs on the caller's stream or on
+ * one of n-1 context-owned streams that fork from and join back into it, so consecutive
+ * chunks overlap.  Each pipeline owns one PC scratch slot. */
+int rsp_set_streams(rsp_ctx* ctx, int32_t n);
+
 /* ---- host-buffer entry points (MEX / fun_MTD_produce drop-in), synchronous ---------- */
 int rsp_pc_mtd(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,
                int64_t P, int64_t R, int64_t batch, float* rdm_out, int32_t rdm_layout);

@@ -38,6 +38,9 @@ struct rsp_ctx {
     rsp::MtdArgs mtd{};
     size_t pc_lds = 0;
     int64_t chunk = 0;  // 0 = default
+    int nstreams = 2;   // chunk pipelines (the caller's stream + nstreams-1 internal ones)
+    hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
     std::vector<void*> owned;           // constant tables (freed at destroy)
     std::map<int, float2*> tw;          // twiddle tables by length
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
@@ -199,6 +202,11 @@ int rsp_destroy(rsp_ctx* ctx) {
         hipEventDestroy(e.a);
         hipEventDestroy(e.b);
     }
+    for (int i = 0; i < 3; ++i) {
+        if (ctx->aux[i]) hipStreamDestroy(ctx->aux[i]);
+        if (ctx->ev_join[i]) hipEventDestroy(ctx->ev_join[i]);
+    }
+    if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return RSP_OK;
@@ -379,6 +387,13 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     rc = twiddles(ctx, (int)p.P, &m.tw);
     if (rc) return bail(rc);
     *out = ctx;
+    return RSP_OK;
+}
+
+int rsp_set_streams(rsp_ctx* ctx, int32_t n) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_streams: null ctx");
+    if (n < 1 || n > 4) return fail(ctx, RSP_ERR_ARG, "rsp_set_streams: n must be 1..4");
+    ctx->nstreams = n;
     return RSP_OK;
 }
 
@@ -577,29 +592,53 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
         m.cv.enabled = 0;
     }
     const int64_t chunk = chunk_of(ctx, batch);
-    int rc = ensure(ctx, ctx->scratch_pc, (size_t)chunk * P * Ro * sizeof(float2));
+    const int64_t nchunks = (batch + chunk - 1) / chunk;
+    const int ns = (int)(ctx->nstreams < nchunks ? ctx->nstreams : nchunks);
+    const size_t cells = (size_t)chunk * P * Ro;   // per chunk slot
+    int rc = ensure(ctx, ctx->scratch_pc, (size_t)ns * cells * sizeof(float2));
     if (rc) return rc;
     if (cfar && !d_flagV) {
-        rc = ensure(ctx, ctx->tmp_flagV, (size_t)chunk * P * Ro);
+        rc = ensure(ctx, ctx->tmp_flagV, (size_t)ns * cells);
         if (rc) return rc;
     }
     if (!d_rdm) {
-        rc = ensure(ctx, ctx->tmp_rdm, (size_t)chunk * P * Ro * sizeof(float));
+        rc = ensure(ctx, ctx->tmp_rdm, (size_t)ns * cells * sizeof(float));
         if (rc) return rc;
     }
-    for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+    // Chunk k runs on lane k % ns (lane 0 = the caller's stream), each lane with its own
+    // scratch slot, so PC of one chunk overlaps MTD / CFAR of the previous one.  The lanes
+    // fork from and join back into the caller's stream.
+    hipStream_t lanes[4] = {s, nullptr, nullptr, nullptr};
+    if (ns > 1) {
+        if (!ctx->ev_fork) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
+        for (int i = 1; i < ns; ++i) {
+            if (!ctx->aux[i - 1]) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->aux[i - 1], hipStreamNonBlocking));
+            if (!ctx->ev_join[i - 1]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_join[i - 1], hipEventDisableTiming));
+            lanes[i] = ctx->aux[i - 1];
+            HIP_TRY(ctx, hipStreamWaitEvent(lanes[i], ctx->ev_fork, 0));
+        }
+    }
+    for (int64_t k = 0; k < nchunks; ++k) {
+        const int64_t c0 = k * chunk;
         const int64_t n = batch - c0 < chunk ? batch - c0 : chunk;
+        const int lane = (int)(k % ns);
+        hipStream_t ls = lanes[lane];
         const char* ein = (const char*)d_echo + (size_t)c0 * P * R * esz;
-        float* rdm = d_rdm ? d_rdm + (size_t)c0 * P * Ro : (float*)ctx->tmp_rdm.p;
+        float* rdm = d_rdm ? d_rdm + (size_t)c0 * P * Ro : (float*)ctx->tmp_rdm.p + lane * cells;
         uint8_t* fv = nullptr;
-        if (cfar) fv = d_flagV ? d_flagV + (size_t)c0 * P * Ro : (uint8_t*)ctx->tmp_flagV.p;
-        float2* pcs = (float2*)ctx->scratch_pc.p;
-        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * P, s));
-        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, s, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, s); }));
+        if (cfar) fv = d_flagV ? d_flagV + (size_t)c0 * P * Ro : (uint8_t*)ctx->tmp_flagV.p + lane * cells;
+        float2* pcs = (float2*)ctx->scratch_pc.p + lane * cells;
+        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * P, ls));
+        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, ls); }));
         if (cfar) {
             uint8_t* fl = d_flag + (size_t)c0 * P * Ro;
-            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, s, [&] { return rsp::launch_cfar_r(rdm, fv, fl, (int)n, cr, s); }));
+            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] { return rsp::launch_cfar_r(rdm, fv, fl, (int)n, cr, ls); }));
         }
+    }
+    for (int i = 1; i < ns; ++i) {
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_join[i - 1], lanes[i]));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join[i - 1], 0));
     }
     return RSP_OK;
 }

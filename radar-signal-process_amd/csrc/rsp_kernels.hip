@@ -203,13 +203,23 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int i = t + G * m;
+#ifdef RSP_AB_NOLOAD
+        u[m] = make_float2((float)(i + row), a.mf.scale);
+#else
         u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
+#endif
     }
     fft_reg<N, G, 1, E>(u, buf, t, tw);
+#ifndef RSP_AB_NOH
 #pragma unroll
     for (int m = 0; m < E; ++m) u[m] = cconj(cmul(u[m], H[t + G * m]));  // conj(X.*H), 1/N in H
+#endif
     fft_reg<N, G, 1, E>(u, buf, t, tw);
+#ifdef RSP_AB_NOSTORE
+    if (u[0].x == 12345.678f) {
+#else
     if (valid) {
+#endif
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int i = t + G * m;

@@ -18,7 +18,7 @@ def _ptr(a):
 
 
 class Engine:
-    def __init__(self, spec, device=0, chunk=0):
+    def __init__(self, spec, device=0, chunk=0, streams=0):
         self.spec = spec
         self.lib = capi.load_library()
         prm, self._keep = spec.to_c()
@@ -29,6 +29,8 @@ class Engine:
         self.device = device
         if chunk:
             self.set_chunk(chunk)
+        if streams:
+            self.set_streams(streams)
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -47,6 +49,9 @@ class Engine:
 
     def __exit__(self, *exc):
         self.close()
+
+    def set_streams(self, n):
+        capi.check(self.lib.rsp_set_streams(self.ctx, int(n)), self.ctx)
 
     def set_chunk(self, cpis):
         capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)
