@@ -141,16 +141,47 @@ hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, con
     return hipGetLastError();
 }
 
+// ================================================================== diagnostic stamps
+// -DRSP_STAMPS builds record s_memtime at phase boundaries of the first NSTAMP_BLOCKS
+// long-segment PC blocks (thread 0); read back with rsp_debug_stamps().  Never in the
+// product build.
+#ifdef RSP_STAMPS
+constexpr int kStampSlots = 8, kStampBlocks = 8192;
+__device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define RSP_STAMP(slot)                                                                    \
+    do {                                                                                   \
+        if (stamp_on) {                                                                    \
+            unsigned long long t_ = stamp_now();                                           \
+            if (threadIdx.x == 0) g_stamps[stamp_blk * kStampSlots + (slot)] = t_;         \
+        }                                                                                  \
+    } while (0)
+#else
+#define RSP_STAMP(slot) do { } while (0)
+#endif
+
 // ================================================================== pulse compression v2
 // One launch per matched-filter segment, specialised on its FFT length N: G threads per
 // PRT row (E = N/G elements each, register-resident Stockham passes), RPB rows per
 // 256..512-thread workgroup.  Row loads and stores are lane-contiguous (the strided
 // element pattern of fft_reg), the spectrum multiply sits between the forward and the
 // inverse FFT in registers, and the only LDS traffic is the inter-pass exchange.
+#ifndef RSP_PC_E
+#define RSP_PC_E 16
+#endif
+#ifndef RSP_PC_WAVES
+#define RSP_PC_WAVES 2
+#endif
 template <int N>
 struct PcCfg {
-    static constexpr int G = N / 16;                            // threads per row
-    static constexpr int E = N / G;                             // 16 elements per thread
+    static constexpr int G = N / RSP_PC_E;                      // threads per row
+    static constexpr int E = N / G;                             // elements per thread
     static constexpr int RPB = G >= 256 ? 1 : 256 / G;          // rows per workgroup
     static constexpr int T = G * RPB;
     static constexpr int SLOT = padded_len(N);
@@ -186,6 +217,11 @@ template <typename TIn, int N, int G>
 __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
                                        const PcMfArgs& a, int row, int t, float2* buf) {
     constexpr int E = N / G;
+#ifdef RSP_STAMPS
+    const bool stamp_on = (N == 4096) && blockIdx.x < kStampBlocks;
+    const int stamp_blk = blockIdx.x;
+#endif
+    RSP_STAMP(0);
     const bool valid = row < a.rows;
     const TIn* x = echo + (size_t)row * a.R;
     float2* y = out + (size_t)row * a.R_out;
@@ -209,12 +245,19 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
 #endif
     }
+#ifdef RSP_STAMPS
+    if (stamp_on) { float acc = 0.f; for (int m = 0; m < E; ++m) acc += u[m].x; asm volatile("" :: "v"(acc)); }
+#endif
+    RSP_STAMP(1);
     fft_reg<N, G, 1, E>(u, buf, t, tw);
+    RSP_STAMP(2);
 #ifndef RSP_AB_NOH
 #pragma unroll
     for (int m = 0; m < E; ++m) u[m] = cconj(cmul(u[m], H[t + G * m]));  // conj(X.*H), 1/N in H
 #endif
+    RSP_STAMP(3);
     fft_reg<N, G, 1, E>(u, buf, t, tw);
+    RSP_STAMP(4);
 #ifdef RSP_AB_NOSTORE
     if (u[0].x == 12345.678f) {
 #else
@@ -226,6 +269,10 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             if (i < out_len) y[out_start + i] = cconj(u[m]);
         }
     }
+#ifdef RSP_STAMPS
+    if (stamp_on) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    RSP_STAMP(5);
 }
 
 // Workgroup size shared by a pair of segment lengths: both run T threads (RPB = T/G rows).
@@ -242,7 +289,7 @@ struct PairCfg {
 // Single segment (N2 == 0) or two independent segments in one launch: blocks
 // [0, nblk2) run segment 2 (the long one, first for a short tail), the rest segment 1.
 template <typename TIn, int N1, int N2>
-__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 4) void pc_mf_kernel(
+__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_PC_WAVES) void pc_mf_kernel(
     const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
@@ -881,3 +928,12 @@ hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, i
 }
 
 }  // namespace rsp
+
+#ifdef RSP_STAMPS
+extern "C" int rsp_debug_stamps(unsigned long long* host, int nblocks) {
+    if (nblocks > rsp::kStampBlocks) nblocks = rsp::kStampBlocks;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(rsp::g_stamps),
+                                    sizeof(unsigned long long) * rsp::kStampSlots * nblocks, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
