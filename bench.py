@@ -89,7 +89,7 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    from rsp import presets, synth
+    from rsp import presets, shard, synth
     from rsp.engine import Engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,7 +106,8 @@ def main():
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
     B, P, R = args.batch, spec.P, spec.R_out
     # contiguous shard of the CPI stream per rank: seed = 1000 + config id 3 + first CPI index
-    echo = synth.echo_torch(spec, B, seed=1003 + rank * B, device=dev, half=args.half)
+    lo, _ = shard.weak_shard(B, rank)
+    echo = synth.echo_torch(spec, B, seed=1003 + lo, device=dev, half=args.half)
     rdm = torch.empty((B, P, R), dtype=torch.float32, device=dev)
     flag = torch.empty((B, P, R), dtype=torch.uint8, device=dev) if cfar else None
     stream = torch.cuda.current_stream(dev)
@@ -134,10 +135,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, device=dev)
 
     # per-kernel device time: an identical pass of `steps` steps with HIP events around every
     # launch (on the launch stream), right after the timed region
