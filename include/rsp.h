@@ -135,8 +135,18 @@ typedef struct {
 const char* rsp_version(void);
 
 /* Create a context bound to HIP device `device` for one parameter set.  Builds the
- * matched-filter spectra (fp64 on the host, stored fp32), twiddle tables and window. */
+ * matched-filter spectra (fp64 on the host, stored fp32), twiddle tables and window.
+ * params == NULL creates a CFAR-only context (rsp_cfar / rsp_cfar_dev). */
 int rsp_create(rsp_ctx** out, int device, const rsp_params* params);
+
+/* Context for fun_MTD_produce v2 built from its `params` fields (MTD/fun_MTD_produce.m:
+ * 34-69, MTD/main_produce_dataset_win_xzr_v2.m:31-45): P = prtNum, R = echo width,
+ * point_prt = {total, p1, p2, p3}, fs [Hz], B [Hz], tao = {tau1, tau2, tau3} [s].
+ * Synthesises pulse2 = exp(j*pi*(-B/tau2)*t^2) and pulse3 = exp(j*pi*(B/tau3)*t^2) with
+ * t = -tau/2 : 1/fs : tau/2-1/fs, the 35-tap FIR /max /1.2 with its 17-sample group-delay
+ * circshift, kaiser(P, 8) + fftshift MTD and fun_0v_pressing /150. */
+int rsp_create_v2(rsp_ctx** out, int device, int64_t P, int64_t R, const int64_t point_prt[4],
+                  double fs, double B, const double tao[3]);
 int rsp_destroy(rsp_ctx* ctx);
 const char* rsp_last_error(const rsp_ctx* ctx);
 

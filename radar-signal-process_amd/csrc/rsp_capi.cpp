@@ -29,6 +29,7 @@ struct DevBuf {
 
 struct rsp_ctx {
     int device = 0;
+    bool cfar_only = false;   // created with params == NULL
     rsp_params p{};
     std::string err;
     hipStream_t stream = nullptr;
@@ -213,8 +214,25 @@ int rsp_destroy(rsp_ctx* ctx) {
 }
 
 int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
-    if (!out || !prm) return fail(nullptr, RSP_ERR_ARG, "rsp_create: null argument");
+    if (!out) return fail(nullptr, RSP_ERR_ARG, "rsp_create: null argument");
     *out = nullptr;
+    if (!prm) {   // CFAR-only context (rsp_cfar / rsp_cfar_dev): a device and a stream
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            return fail(nullptr, RSP_ERR_HIP, "rsp_create: no HIP device available");
+        if (device < 0 || device >= ndev)
+            return fail(nullptr, RSP_ERR_ARG, "rsp_create: device %d out of range (%d devices)", device, ndev);
+        rsp_ctx* ctx = new rsp_ctx();
+        ctx->device = device;
+        ctx->cfar_only = true;
+        if (hipSetDevice(device) != hipSuccess ||
+            hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete ctx;
+            return fail(nullptr, RSP_ERR_HIP, "rsp_create: device/stream setup failed");
+        }
+        *out = ctx;
+        return RSP_OK;
+    }
     const rsp_params& p = *prm;
     if (p.P < 2 || p.R < 1 || p.R_out < 1 || p.R > (1 << 24) || p.R_out > (1 << 24))
         return fail(nullptr, RSP_ERR_SHAPE, "rsp_create: bad P=%lld R=%lld R_out=%lld",
@@ -390,6 +408,79 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     return RSP_OK;
 }
 
+// MTD/fun_lss_pulse_compression.m:31 (also DMX_SignalProcessing_main_xzr.m:146)
+static const double kFirTaps[35] = {-9, -7, -2, 10, 27, 40, 42, 24, -13, -57, -89, -86, -30, 77, 220, 364, 471, 511,
+                                    471, 364, 220, 77, -30, -86, -89, -57, -13, 24, 42, 40, 27, 10, -2, -7, -9};
+
+static int64_t colon_count(double a, double d, double b) {   // MATLAB a:d:b length
+    const double q = (b - a) / d;
+    const double r = std::floor(q + 0.5);
+    return (std::fabs(q - r) < 1e-9 * (std::fabs(q) > 1 ? std::fabs(q) : 1.0) ? (int64_t)r : (int64_t)std::floor(q)) + 1;
+}
+
+static int64_t nextpow2(int64_t n) {
+    int64_t p = 64;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+int rsp_create_v2(rsp_ctx** out, int device, int64_t P, int64_t R, const int64_t point_prt[4], double fs,
+                  double B, const double tao[3]) {
+    if (!out || !point_prt || !tao || fs <= 0 || tao[1] <= 0 || tao[2] <= 0)
+        return fail(nullptr, RSP_ERR_ARG, "rsp_create_v2: bad argument");
+    const int64_t p1 = point_prt[1], p2 = point_prt[2], p3 = point_prt[3];
+    if (p1 < 1 || p2 < 1 || p3 < 1 || p1 + p2 + p3 > R)
+        return fail(nullptr, RSP_ERR_SHAPE, "rsp_create_v2: point_prt segments exceed R=%lld", (long long)R);
+    const double ts = 1.0 / fs;
+    std::vector<double> re[2], im[2];
+    for (int k = 0; k < 2; ++k) {   // pulse2 (K = -B/tau2), pulse3 (K = +B/tau3): fun_MTD_produce.m:62-69
+        const double tau = tao[k + 1], K = (k == 0 ? -B : B) / tau;
+        const int64_t n = colon_count(-tau / 2, ts, tau / 2 - ts);
+        re[k].resize((size_t)n);
+        im[k].resize((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            const double t = -tau / 2 + ts * (double)i;
+            const double ph = 2.0 * M_PI * 0.5 * K * t * t;
+            re[k][i] = std::cos(ph);
+            im[k][i] = std::sin(ph);
+        }
+    }
+    std::vector<double> taps(35);
+    for (int i = 0; i < 35; ++i) taps[i] = kFirTaps[i] / 511.0;   // filter_coef / max (:32)
+    rsp_params prm;
+    std::memset(&prm, 0, sizeof(prm));
+    prm.P = P;
+    prm.R = R;
+    prm.R_out = R;
+    prm.nseg = 3;
+    prm.window = RSP_WIN_KAISER;
+    prm.window_beta = 8.0;
+    prm.fftshift = 1;
+    prm.zero_v_div = 150;
+    rsp_pc_segment& a = prm.seg[0];
+    a.kind = RSP_SEG_FIR;
+    a.fir_shift = 17;   // round(mean(grpdelay(b))) of the symmetric 35-tap FIR (:47)
+    a.in_start = 0;
+    a.in_len = a.out_len = p1;
+    a.scale = 1.0 / 1.2;
+    a.coef_len = 35;
+    a.coef_re = taps.data();
+    const int64_t m3 = R - p1 - p2;
+    for (int k = 0; k < 2; ++k) {
+        rsp_pc_segment& g = prm.seg[k + 1];
+        g.kind = RSP_SEG_MF;
+        g.in_start = g.out_start = k == 0 ? p1 : p1 + p2;
+        g.in_len = k == 0 ? p2 : m3;
+        g.out_len = k == 0 ? p2 : p3;
+        g.coef_len = (int64_t)re[k].size();
+        g.nfft = nextpow2(g.in_len + g.coef_len - 1);
+        g.scale = 1.0;
+        g.coef_re = re[k].data();
+        g.coef_im = im[k].data();
+    }
+    return rsp_create(out, device, &prm);
+}
+
 int rsp_set_streams(rsp_ctx* ctx, int32_t n) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_streams: null ctx");
     if (n < 1 || n > 4) return fail(ctx, RSP_ERR_ARG, "rsp_set_streams: n must be 1..4");
@@ -563,6 +654,7 @@ int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches) {
 
 int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, void* d_pc, void* stream) {
     if (!ctx || !d_echo || !d_pc || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: bad argument");
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "context was created for CFAR only (params == NULL)");
     if (dtype != RSP_C64 && dtype != RSP_C32F16) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: dtype %d", dtype);
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
     HIP_TRY(ctx, run_pc(ctx, d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, (hipStream_t)stream));
@@ -573,6 +665,7 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
                         const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
                         void* stream) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: null ctx");
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "context was created for CFAR only (params == NULL)");
     if (!d_echo || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: bad echo/batch");
     if (dtype != RSP_C64 && dtype != RSP_C32F16)
         return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: device dtype must be RSP_C64 or RSP_C32F16");
@@ -727,6 +820,7 @@ static int fetch(rsp_ctx* ctx, const T* d, T* h, int64_t batch, int64_t A, int64
 
 static int check_host_call(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P,
                            int64_t R, int64_t batch) {
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "context was created for CFAR only (params == NULL)");
     if (!echo || batch < 0) return fail(ctx, RSP_ERR_ARG, "null echo or negative batch");
     if (!dtype_size(dtype)) return fail(ctx, RSP_ERR_ARG, "bad dtype %d", dtype);
     if (layout != RSP_ROWMAJOR && layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad layout %d", layout);

@@ -1,0 +1,76 @@
+/*
+ * executeCFAR_mex.c -- MEX drop-in for
+ *   [flag, flagV] = executeCFAR(rdm, refR, saveR, TR, mR, refV, saveV, TV, mV, M0, rFlag)
+ * (MatlabProcess_xuzerui/CFAR_WangCai/executeCFAR.m:1-2).  fun_CFARflag is a local
+ * function of main_cfar.m (:142) and cannot be shadowed, so the interposition point is
+ * executeCFAR, which fun_CFARflag calls once per column segment (:147-154).
+ *
+ * Build:  mex -R2018a -I<repo>/include executeCFAR_mex.c \
+ *             -L<repo>/radar-signal-process_amd/lib -lrsp -output executeCFAR
+ * rdm: V x R real double (column-major, converted to fp32 for the GPU).  Outputs are
+ * V x R double 0/1 like the reference.  A CFAR window that does not fit raises
+ * rsp:cfar_window, as MATLAB's index error would.
+ */
+#include <string.h>
+
+#include "mex.h"
+#include "rsp.h"
+
+static rsp_ctx* g_ctx = NULL;
+
+static void cleanup(void) {
+    if (g_ctx) rsp_destroy(g_ctx);
+    g_ctx = NULL;
+}
+
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs != 11)
+        mexErrMsgIdAndTxt("rsp:usage", "[flag, flagV] = executeCFAR(rdm, refR, saveR, TR, mR, refV, saveV, TV, mV, M0, rFlag)");
+    const mxArray* M = prhs[0];
+    if (!mxIsDouble(M) || mxIsComplex(M)) mexErrMsgIdAndTxt("rsp:rdm", "rdm must be real double");
+    const int64_t V = (int64_t)mxGetM(M), R = (int64_t)mxGetN(M);
+    rsp_cfar_params cf;
+    memset(&cf, 0, sizeof(cf));
+    cf.refR = (int32_t)mxGetScalar(prhs[1]);
+    cf.saveR = (int32_t)mxGetScalar(prhs[2]);
+    cf.TR = mxGetScalar(prhs[3]);
+    cf.methodR = (int32_t)mxGetScalar(prhs[4]);
+    cf.refV = (int32_t)mxGetScalar(prhs[5]);
+    cf.saveV = (int32_t)mxGetScalar(prhs[6]);
+    cf.TV = mxGetScalar(prhs[7]);
+    cf.methodV = (int32_t)mxGetScalar(prhs[8]);
+    cf.M0 = (int32_t)mxGetScalar(prhs[9]);
+    cf.rFlag = mxGetScalar(prhs[10]) != 0.0;
+    cf.zero_v_div = 0;
+    cf.nseg = 0;
+    if (!g_ctx) {
+        if (rsp_create(&g_ctx, 0, NULL) != RSP_OK) {
+            g_ctx = NULL;
+            mexErrMsgIdAndTxt("rsp:create", "%s", rsp_last_error(NULL));
+        }
+        mexAtExit(cleanup);
+    }
+    const size_t n = (size_t)(V * R);
+    const double* in = mxGetDoubles(M);
+    float* r32 = (float*)mxMalloc(n * sizeof(float));
+    uint8_t* f = (uint8_t*)mxMalloc(n);
+    uint8_t* fv = (uint8_t*)mxMalloc(n);
+    for (size_t i = 0; i < n; ++i) r32[i] = (float)in[i];
+    int rc = rsp_cfar(g_ctx, r32, RSP_COLMAJOR, V, R, 1, &cf, f, fv);
+    if (rc != RSP_OK) {
+        char msg[512];
+        strncpy(msg, rsp_last_error(g_ctx), sizeof(msg) - 1);
+        msg[sizeof(msg) - 1] = 0;
+        mxFree(r32); mxFree(f); mxFree(fv);
+        mexErrMsgIdAndTxt(rc == RSP_ERR_CFAR_WINDOW ? "rsp:cfar_window" : "rsp:run", "%s", msg);
+    }
+    plhs[0] = mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL);
+    double* o = mxGetDoubles(plhs[0]);
+    for (size_t i = 0; i < n; ++i) o[i] = f[i];
+    if (nlhs > 1) {
+        plhs[1] = mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL);
+        double* ov = mxGetDoubles(plhs[1]);
+        for (size_t i = 0; i < n; ++i) ov[i] = fv[i];
+    }
+    mxFree(r32); mxFree(f); mxFree(fv);
+}

@@ -27,7 +27,8 @@ RSP_WIN_KAISER, RSP_WIN_HAMMING, RSP_WIN_RECT = 0, 1, 2
 # Every exported symbol of include/rsp.h (checked by tests/test_capi_cpu.py)
 EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_set_chunk",
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
-           "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams")
+           "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
+           "rsp_create_v2")
 RSP_NKERNELS = 4
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
 
@@ -99,6 +100,9 @@ def load_library(path=None):
     lib.rsp_cfar_dev.argtypes = [vp, vp, i64, i64, i64, C.POINTER(rsp_cfar_params), vp, vp, vp]
     lib.rsp_pc_dev.restype = C.c_int
     lib.rsp_pc_dev.argtypes = [vp, vp, i32, i64, vp, vp]
+    lib.rsp_create_v2.restype = C.c_int
+    lib.rsp_create_v2.argtypes = [C.POINTER(vp), C.c_int, i64, i64, C.POINTER(i64), C.c_double, C.c_double,
+                                  C.POINTER(C.c_double)]
     lib.rsp_set_streams.restype = C.c_int
     lib.rsp_set_streams.argtypes = [vp, i32]
     lib.rsp_profile.restype = C.c_int

@@ -19,11 +19,14 @@ def _ptr(a):
 
 class Engine:
     def __init__(self, spec, device=0, chunk=0, streams=0):
-        self.spec = spec
+        self.spec = spec          # None: CFAR-only context
         self.lib = capi.load_library()
-        prm, self._keep = spec.to_c()
         ctx = C.c_void_p()
-        rc = self.lib.rsp_create(C.byref(ctx), int(device), C.byref(prm))
+        if spec is None:
+            rc = self.lib.rsp_create(C.byref(ctx), int(device), None)
+        else:
+            prm, self._keep = spec.to_c()
+            rc = self.lib.rsp_create(C.byref(ctx), int(device), C.byref(prm))
         capi.check(rc, None)
         self.ctx = ctx
         self.device = device

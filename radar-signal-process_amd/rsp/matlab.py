@@ -66,8 +66,8 @@ def fun_MTD_produce_legacy(echo, device=0):
 
 
 def _cfar_engine(device=0):
-    # rsp_cfar needs a context only for its device and buffers; any small spec will do
-    return _engine(("cfar-only",), lambda: presets.dmx(16, 64), device)
+    # rsp_cfar needs a context only for its device and buffers: rsp_create(params=NULL)
+    return _engine(("cfar-only",), lambda: None, device)
 
 
 def executeCFAR(echo_MTD, refCells_R, saveCells_R, T_CFAR_R, CFARmethod_R, refCells_V, saveCells_V,

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _header_functions():
     text = open(os.path.join(ROOT, "include", "rsp.h")).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(rsp_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(rsp_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_header():

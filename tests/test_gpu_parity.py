@@ -266,3 +266,26 @@ def test_full_batch_properties(torch_cuda):
     torch.cuda.synchronize()
     assert torch.equal(rdm2, rdm * 2.0)
     assert torch.equal(flag2, flag)
+
+
+def test_create_v2_matches_python_preset(torch_cuda):
+    """rsp_create_v2 (the MEX path: params fields -> context in C) == the Python v2 preset."""
+    import ctypes as C
+    from rsp import _capi as capi, presets, synth
+    from rsp.engine import Engine
+    P, R = 64, 1024
+    lib = capi.load_library()
+    ctx = C.c_void_p()
+    pp = (C.c_int64 * 4)(R, 228, 723, R - 951)
+    tao = (C.c_double * 3)(0.16e-6, 8e-6, 28e-6)
+    assert lib.rsp_create_v2(C.byref(ctx), 0, P, R, pp, 25e6, 20e6, tao) == 0
+    echo = synth.echo_numpy(presets.v2(P, R), 2, seed=9).astype(np.complex128)
+    out = np.empty((2, P, R), np.float32)
+    rc = lib.rsp_pc_mtd(ctx, echo.ctypes.data, capi.RSP_C128, capi.RSP_ROWMAJOR, P, R, 2, out.ctypes.data,
+                        capi.RSP_ROWMAJOR)
+    assert rc == 0
+    lib.rsp_destroy(ctx)
+    with Engine(presets.v2(P, R)) as eng:
+        want = eng.pc_mtd(echo)
+    assert rel_err(out, want) < 1e-6
+    assert rel_err(out, oracle_rdm("v2", echo)) < RDM_TOL
