@@ -17,11 +17,49 @@ namespace rsp {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+// Packed-FP32 complex primitives.  gfx950's VOP3P v_pk_* instructions take per-half
+// operand selects (op_sel / op_sel_hi) and negations (neg_lo / neg_hi), so a (+-j) rotation
+// folded into an add, or a complex product, needs no register shuffles.  hipcc does not
+// emit the negation modifiers on its own (it spends v_xor + v_mov per rotation), hence the
+// inline asm; -DRSP_NO_ASM selects the portable forms.
+#ifndef RSP_NO_ASM
+// a + (-j) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ float2 add_mj(float2 a, float2 b) {
+    float2 d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+// a + j b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ float2 add_pj(float2 a, float2 b) {
+    float2 d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+// a * b in two instructions: m = (-a.y b.y, a.y b.x); d = (a.x b.x, a.x b.y) + m
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    float2 m, d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]" : "=v"(m) : "v"(a), "v"(b));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(d) : "v"(a), "v"(b), "v"(m));
+    return d;
+}
+// conj(a * b) in two instructions (negated high half of the fma)
+__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {
+    float2 m, d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]" : "=v"(m) : "v"(a), "v"(b));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(b), "v"(m));
+    return d;
+}
+#else
+__device__ __forceinline__ float2 add_mj(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
+__device__ __forceinline__ float2 add_pj(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
-__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) { return cconj(cmul(a, b)); }
+#endif
 // a * (-j)
 __device__ __forceinline__ float2 cmul_mj(float2 a) { return make_float2(a.y, -a.x); }
 
@@ -37,12 +75,22 @@ __device__ __forceinline__ void dft2(float2& a, float2& b) {
 }
 
 __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
-    float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
-    float2 t2 = cadd(a1, a3), t3 = cmul_mj(csub(a1, a3));
+    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    const float2 t2 = cadd(a1, a3), d = csub(a1, a3);
     a0 = cadd(t0, t2);
     a2 = csub(t0, t2);
-    a1 = cadd(t1, t3);
-    a3 = csub(t1, t3);
+    a1 = add_mj(t1, d);   // t1 + (-j) d
+    a3 = add_pj(t1, d);   // t1 - (-j) d
+}
+
+// DFT4 of (a0, a1, -j*a2, a3): the W16^4 = -j twiddle folded into the first butterfly
+__device__ __forceinline__ void dft4_a2mj(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = add_mj(a0, a2), t1 = add_pj(a0, a2);
+    const float2 t2 = cadd(a1, a3), d = csub(a1, a3);
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = add_mj(t1, d);
+    a3 = add_pj(t1, d);
 }
 
 __device__ __forceinline__ void dft3(float2& a0, float2& a1, float2& a2) {
@@ -63,13 +111,12 @@ __device__ __forceinline__ void dft8(float2* v) {
     float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
     dft4(e0, e1, e2, e3);
     dft4(o0, o1, o2, o3);
-    // o_k *= W8^k
-    o1 = make_float2(h * (o1.x + o1.y), h * (o1.y - o1.x));
-    o2 = cmul_mj(o2);
-    o3 = make_float2(h * (o3.y - o3.x), -h * (o3.x + o3.y));
+    // o_k *= W8^k (W8^2 = -j folded into the adds)
+    o1 = cmul(o1, make_float2(h, -h));
+    o3 = cmul(o3, make_float2(-h, -h));
     v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
     v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
-    v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
+    v[2] = add_mj(e2, o2); v[6] = add_pj(e2, o2);
     v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
 }
 
@@ -82,20 +129,21 @@ __device__ __forceinline__ void dft16(float2* v) {
     // v[4*k1 + n2] now holds b[n2][k1]; multiply by W16^(n2*k1)
     // n2=1: k1=1..3 -> W^1, W^2, W^3 ; n2=2: W^2, W^4, W^6 ; n2=3: W^3, W^6, W^9
     v[5] = cmul(v[5], make_float2(c1, -s1));
-    v[9] = make_float2(h * (v[9].x + v[9].y), h * (v[9].y - v[9].x));
+    v[9] = cmul(v[9], make_float2(h, -h));
     v[13] = cmul(v[13], make_float2(s1, -c1));
-    v[6] = make_float2(h * (v[6].x + v[6].y), h * (v[6].y - v[6].x));
-    v[10] = cmul_mj(v[10]);
-    v[14] = make_float2(h * (v[14].y - v[14].x), -h * (v[14].x + v[14].y));
+    v[6] = cmul(v[6], make_float2(h, -h));
+    // v[10] *= W16^4 = -j: folded into dft4_a2mj below
+    v[14] = cmul(v[14], make_float2(-h, -h));
     v[7] = cmul(v[7], make_float2(s1, -c1));
-    v[11] = make_float2(h * (v[11].y - v[11].x), -h * (v[11].x + v[11].y));
+    v[11] = cmul(v[11], make_float2(-h, -h));
     v[15] = cmul(v[15], make_float2(-c1, s1));
     // second stage: for each k1, DFT4 over n2 of v[4*k1 + n2] -> X[k1 + 4*k2]
     float2 x[16];
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1) {
         float2 a0 = v[4 * k1 + 0], a1 = v[4 * k1 + 1], a2 = v[4 * k1 + 2], a3 = v[4 * k1 + 3];
-        dft4(a0, a1, a2, a3);
+        if (k1 == 2) dft4_a2mj(a0, a1, a2, a3);
+        else dft4(a0, a1, a2, a3);
         x[k1] = a0; x[k1 + 4] = a1; x[k1 + 8] = a2; x[k1 + 12] = a3;
     }
 #pragma unroll

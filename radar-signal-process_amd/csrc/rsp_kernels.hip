@@ -253,7 +253,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     RSP_STAMP(2);
 #ifndef RSP_AB_NOH
 #pragma unroll
-    for (int m = 0; m < E; ++m) u[m] = cconj(cmul(u[m], H[t + G * m]));  // conj(X.*H), 1/N in H
+    for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], H[t + G * m]);  // conj(X.*H), 1/N in H
 #endif
     RSP_STAMP(3);
     fft_reg<N, G, 1, E>(u, buf, t, tw);
