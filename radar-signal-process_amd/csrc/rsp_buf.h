@@ -1,0 +1,35 @@
+// Raw buffer access for gfx950 (device code only).
+//
+// A buffer resource (V#) covers one CPI plane; lanes address it with a 32-bit per-lane
+// voffset plus a wave-uniform soffset, so strided slow-time / Doppler-row accesses put
+// their row stride in an SGPR and spend no VALU on 64-bit address arithmetic.  The
+// hardware range check (offset >= num_records) makes loads return 0 and drops stores,
+// which replaces per-element `if (in range)` branches: a lane that must not touch memory
+// uses kOob as its voffset.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsp {
+
+constexpr int kBufWord3 = 0x00020000;    // gfx9 resource word 3 (raw, 32-bit data format)
+constexpr uint32_t kOob = 0x80000000u;   // voffset beyond any plane (planes are < 2 GiB)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, kBufWord3);
+}
+
+__device__ __forceinline__ float2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ float buf_ld_f(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st_f(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_st_u8(uint8_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, voff, soff, 0);
+}
+
+}  // namespace rsp

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rsp_fft.h"
+#include "rsp_buf.h"
 #include "rsp_internal.h"
 
 namespace rsp {
@@ -451,13 +452,74 @@ struct MtdCfg {
     static constexpr int W = kBlock / G;               // range bins per workgroup
     static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
     static constexpr int MS = P + 1;                   // odd float stride of a CFAR column
+    static constexpr int SPAD = 32;                    // sums pad: save + ref + 2 <= 32 (host-checked)
+    static constexpr int SMS = P + 2 * SPAD + 1;       // padded sums column (odd stride)
     static constexpr size_t lds_fft = (size_t)W * SLOT * sizeof(float2);
-    static constexpr size_t lds_cfar = (size_t)2 * W * MS * sizeof(float);
+    static constexpr size_t lds_cfar = (size_t)W * (MS + SMS) * sizeof(float);
     static constexpr size_t lds = lds_fft > lds_cfar ? lds_fft : lds_cfar;
     static_assert(G * E == P && (G & (G - 1)) == 0 && G <= kBlock, "MTD tiling");
 };
 
-template <int P>
+// Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
+// guard `save` and the row band stay runtime).  The thread's run of E rows plus REF-1
+// look-ahead rows is read from LDS once; its E window sums are direct left-to-right adds
+// (the order mean() uses) and go to a padded sums column, so the left/right window lookups
+// of every row are unclamped LDS reads with immediate offsets.
+template <int P, int REF, bool GO>
+__device__ __forceinline__ void doppler_rows_fixed(const float* m, const float* sums, const CfarVArgs& cv,
+                                                   bool col_on, int v0, __amdgpu_buffer_rsrc_t out,
+                                                   uint32_t vo, uint32_t R) {
+    constexpr int E = MtdCfg<P>::E;
+    const int kl = cv.lo + cv.save + REF - v0;     // row v0+i has a left window iff i >= kl
+    const int kr = cv.hi - cv.save - 1 - REF - v0; // ... and a right window iff i <= kr
+    const int b0 = cv.lo - v0, b1 = cv.hi - v0;    // tested rows: b0 <= i < b1
+    const float* sl_p = sums + v0 - cv.save - REF;
+    const float* sr_p = sums + v0 + cv.save + 1;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        const float sl = sl_p[i], sr = sr_p[i];    // pad / other rows when unused: selected away
+        const bool lok = i >= kl, rok = i <= kr;
+        const float x = lok ? sl : sr, y = rok ? sr : sl;   // one-sided fallback (:30-39)
+        // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
+        const float th = (GO ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
+        const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
+        buf_st_u8(hit ? 1 : 0, out, vo, (uint32_t)i * R);
+    }
+}
+
+// Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
+// guard `save`, the method and the row band stay runtime).  The thread's run of E rows plus
+// REF-1 look-ahead rows is read from LDS once; its E window sums are direct left-to-right
+// adds (the order mean() uses) and go to a padded sums column, so every row's left/right
+// window lookups are unclamped LDS reads with immediate offsets.
+template <int P, int REF>
+__device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums, const CfarVArgs& cv,
+                                                   bool col_on, int v0, __amdgpu_buffer_rsrc_t out,
+                                                   uint32_t vo, uint32_t R) {
+    constexpr int E = MtdCfg<P>::E;
+    float m[E + REF - 1];
+#pragma unroll
+    for (int i = 0; i < E + REF - 1; ++i) m[i] = mag[v0 + i];   // rows >= P: unused garbage
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        float acc = m[i];
+#pragma unroll
+        for (int k = 1; k < REF; ++k) acc += m[i + k];
+        sums[v0 + i] = acc;
+    }
+    __syncthreads();
+    if (cv.method == 0) doppler_rows_fixed<P, REF, true>(m, sums, cv, col_on, v0, out, vo, R);
+    else doppler_rows_fixed<P, REF, false>(m, sums, cv, col_on, v0, out, vo, R);
+}
+
+// MTD: one workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the
+// tile, pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
+// samples load straight into registers with W-wide coalesced rows, the slow-time FFT runs
+// register-resident with LDS exchanges, and |X| leaves in coalesced RDM rows.  The fftshift
+// offset is 0 or P/2, a multiple of G, so bin g + G*m lands in row g + G*((m + shift/G) mod E):
+// a wave-uniform rotation, and every row offset is an SGPR operand of the buffer access.
+// REF > 0: Doppler CFAR specialised on the reference window; REF == 0: runtime window.
+template <int P, int REF>
 __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
@@ -466,65 +528,88 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int c = threadIdx.x % W, g = threadIdx.x / W;
     const size_t cpi = blockIdx.y;
-    const int R = a.R_out;
+    const uint32_t R = (uint32_t)a.R_out;
     const int r = blockIdx.x * W + c;
-    const bool rv = r < R;
-    const float2* src = pc + cpi * (size_t)P * R + (rv ? r : 0);
+    const bool rv = r < (int)R;
+    const uint32_t plane = (uint32_t)P * R;
+    const uint32_t cell = (uint32_t)g * R + (uint32_t)r;        // element (g, r) of a plane
+    const auto src = buf_rsrc(pc + cpi * plane, plane * 8u);
+    const uint32_t vo_in = rv ? cell * 8u : kOob;
     float2 u[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        const int p = g + G * m;
-        const float2 v = rv ? src[(size_t)p * R] : make_float2(0.f, 0.f);
-        const float w = a.win[p];
+        const float2 v = buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u);
+        const float w = a.win[g + G * m];
         u[m] = make_float2(v.x * w, v.y * w);
     }
     fft_reg<P, G, 1, E>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, a.tw);
 
-    float* dst = rdm + cpi * (size_t)P * R + r;
+    const auto dst = buf_rsrc(rdm + cpi * plane, plane * 4u);
+    const uint32_t vo_out = rv ? cell * 4u : kOob;
+    const int srot = a.shift / G;
     float mg[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        const int q = g + G * m;          // FFT bin
-        int v = q + a.shift;              // fftshift: out[v] = X[(v - shift) mod P]
-        if (v >= P) v -= P;
-        float mm = sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
-        if (v >= a.z_lo && v < a.z_hi) mm = 0.f;   // fun_0v_pressing
-        mg[m] = mm;
-        if (rv) dst[(size_t)v * R] = mm;
+        int mm = m + srot;                // fftshift: bin g + G*m -> row g + G*mm
+        if (mm >= E) mm -= E;
+        const int v = g + G * mm;
+        float x = __builtin_amdgcn_sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
+        if (v >= a.z_lo && v < a.z_hi) x = 0.f;   // fun_0v_pressing
+        mg[m] = x;
+        buf_st_f(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
     if (!a.cv.enabled) return;
     __syncthreads();  // the FFT exchange slots are free from here on
     float* mag = reinterpret_cast<float*>(smem) + c * C::MS;
-    float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::MS;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        const int q = g + G * m;
-        int v = q + a.shift;
-        if (v >= P) v -= P;
+        int mm = m + srot;
+        if (mm >= E) mm -= E;
+        const int v = g + G * mm;
         mag[v] = (v >= a.cv.cz_lo && v < a.cv.cz_hi) ? 0.f : mg[m];   // main_cfar.m:90-91
     }
     __syncthreads();
-    const int v0 = g * E, v1 = v0 + E;   // this thread's run of Doppler rows
-    doppler_sums(mag, sums, P, a.cv.ref, v0, v1);
-    __syncthreads();
+    const int v0 = g * E;   // this thread's run of Doppler rows
     const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
-    doppler_flags(mag, sums, a.cv, col_on, v0, v1, flagV + cpi * (size_t)P * R + r, R, rv);
+    if constexpr (REF > 0) {
+        float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
+        const auto fo = buf_rsrc(flagV + cpi * plane, plane);
+        doppler_cfar_fixed<P, REF>(mag, sums, a.cv, col_on, v0, fo, rv ? (uint32_t)v0 * R + r : kOob, R);
+    } else {
+        float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
+        doppler_sums(mag, sums, P, a.cv.ref, v0, v0 + E);
+        __syncthreads();
+        doppler_flags(mag, sums, a.cv, col_on, v0, v0 + E, flagV + cpi * (size_t)P * R + r, R, rv);
+    }
+}
+
+template <int P, int REF>
+static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
+                                const MtdArgs& a, hipStream_t s) {
+    using C = MtdCfg<P>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P, REF>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi), block(kBlock);
+    hipLaunchKernelGGL((mtd_kernel<P, REF>), grid, block, C::lds, s, pc, rdm, flagV, a);
+    return hipGetLastError();
 }
 
 template <int P>
 static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi), block(kBlock);
-    hipLaunchKernelGGL(mtd_kernel<P>, grid, block, C::lds, s, pc, rdm, flagV, a);
-    return hipGetLastError();
+    // shift is 0 or floor(P/2) = G*E/2; the row rotation needs it to be a multiple of G,
+    // and the padded sums column needs save + ref + 2 <= SPAD
+    if (a.shift % C::G != 0 || a.shift < 0 || a.shift >= P) return hipErrorInvalidValue;
+    if (a.cv.enabled && a.cv.save + a.cv.ref + 2 > C::SPAD) return hipErrorInvalidValue;
+    if ((uint64_t)P * a.R_out * 8 >= (uint64_t)kOob) return hipErrorInvalidValue;
+    if (a.cv.enabled && a.cv.ref == 5) return launch_mtd_pr<P, 5>(pc, rdm, flagV, ncpi, a, s);
+    return launch_mtd_pr<P, 0>(pc, rdm, flagV, ncpi, a, s);
 }
 
 bool mtd_size_supported(int P) {
