@@ -190,7 +190,9 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
 
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
- * every kernel while profiling is enabled (enable = 1 also resets the counters).
+ * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1
+ * every N-th launch (sampling: each event pair costs the stream a few microseconds),
+ * 0 stops.  Any call resets the counters.
  * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V. */
 #define RSP_NKERNELS 4
 enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3 };

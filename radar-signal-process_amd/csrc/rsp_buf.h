@@ -7,6 +7,7 @@
 // which replaces per-element `if (in range)` branches: a lane that must not touch memory
 // uses kOob as its voffset.
 #pragma once
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,11 +26,23 @@ __device__ __forceinline__ float2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, uint32_t v
 __device__ __forceinline__ float buf_ld_f(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
+__device__ __forceinline__ void buf_st_f2(float2 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    typedef int v2i __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), r, voff, soff, 0);
+}
 __device__ __forceinline__ void buf_st_f(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
 }
 __device__ __forceinline__ void buf_st_u8(uint8_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b8(v, r, voff, soff, 0);
+}
+
+// one complex element of an input plane (complex fp32, or fp16 I/Q widened on load)
+__device__ __forceinline__ float2 buf_ld_c(const float2*, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return buf_ld_f2(r, voff, soff);
+}
+__device__ __forceinline__ float2 buf_ld_c(const __half2*, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0)));
 }
 
 }  // namespace rsp

@@ -51,7 +51,8 @@ struct rsp_ctx {
         int k;
         hipEvent_t a, b;
     };
-    bool prof = false;
+    int prof = 0;            // 0 off; N >= 1: bracket every N-th launch
+    uint64_t prof_tick = 0;
     std::vector<Ev> evs;
     size_t nev = 0;
     double prof_ms[RSP_NKERNELS] = {};
@@ -586,10 +587,13 @@ static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSu
 
 static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s);
 
-// Run one kernel launch, bracketed by HIP events on `s` when profiling is on.
+// Run one kernel launch, bracketed by HIP events on `s` when profiling is on (every
+// ctx->prof-th launch: a timing event costs the stream a few microseconds, so a sampled
+// bracket keeps the measured region's throughput unchanged).
 template <typename F>
 static hipError_t timed(rsp_ctx* ctx, int k, hipStream_t s, F&& launch) {
     if (!ctx->prof) return launch();
+    if (ctx->prof_tick++ % (uint64_t)ctx->prof != 0) return launch();
     if (ctx->nev == ctx->evs.size()) {
         rsp_ctx::Ev e{k, nullptr, nullptr};
         hipError_t r = hipEventCreate(&e.a);
@@ -625,7 +629,9 @@ static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, 
 
 int rsp_profile(rsp_ctx* ctx, int32_t enable) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_profile: null ctx");
-    ctx->prof = enable != 0;
+    if (enable < 0) return fail(ctx, RSP_ERR_ARG, "rsp_profile: enable %d < 0", enable);
+    ctx->prof = enable;
+    ctx->prof_tick = 0;
     ctx->nev = 0;
     for (int k = 0; k < RSP_NKERNELS; ++k) {
         ctx->prof_ms[k] = 0;

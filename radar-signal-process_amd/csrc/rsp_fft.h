@@ -15,8 +15,6 @@
 
 namespace rsp {
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 
@@ -26,6 +24,19 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 // emit the negation modifiers on its own (it spends v_xor + v_mov per rotation), hence the
 // inline asm; -DRSP_NO_ASM selects the portable forms.
 #ifndef RSP_NO_ASM
+// Plain add/sub as packed asm too: left to itself the SLP vectorizer pairs lanes of
+// *different* complex values, (a.x + b.x, c.x + d.x), and then shuffles them back with
+// v_mov into the (re, im) pairs the other primitives take.
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+    float2 d;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+    float2 d;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
 // a + (-j) b = (a.x + b.y, a.y - b.x)
 __device__ __forceinline__ float2 add_mj(float2 a, float2 b) {
     float2 d;
@@ -53,6 +64,8 @@ __device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {
     return d;
 }
 #else
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 add_mj(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
 __device__ __forceinline__ float2 add_pj(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -348,6 +361,133 @@ __device__ __forceinline__ void fft_reg(float2 (&u)[E], float2* buf, int t, cons
             __syncthreads();  // RAW
         }
         fft_reg<N, G, Ns * R, E>(u, buf, t, tw);
+    }
+}
+
+
+// ---------------------------------------------------------------- preloaded twiddles
+// The inverse transform is conj(FFT(conj(.))), so forward and inverse passes use the
+// same twiddle entries: a thread loads its per-pass twiddles once (tw_preload, issued
+// together with the row's input loads so their latency overlaps) and every pass reads
+// them from registers instead of waiting on table loads after each LDS exchange.
+__host__ __device__ constexpr int tw_loads(int R) { return R == 16 ? 6 : R == 8 ? 4 : R - 1; }
+
+template <int N, int E>
+__host__ __device__ constexpr int tw_regs(int Ns = 1) {
+    int total = 0;
+    while (Ns < N) {
+        const int R = pick_radix_e(N / Ns, E);
+        if (Ns > 1) total += (E / R) * tw_loads(R);
+        Ns *= R;
+    }
+    return total;
+}
+
+template <int R>
+__device__ __forceinline__ void tw_fetch(float2* w, int e, const float2* __restrict__ tw) {
+    if constexpr (R == 16) {
+        w[0] = tw[e]; w[1] = tw[2 * e]; w[2] = tw[3 * e];
+        w[3] = tw[4 * e]; w[4] = tw[8 * e]; w[5] = tw[12 * e];
+    } else if constexpr (R == 8) {
+        w[0] = tw[e]; w[1] = tw[2 * e]; w[2] = tw[3 * e]; w[3] = tw[4 * e];
+    } else {
+#pragma unroll
+        for (int r = 1; r < R; ++r) w[r - 1] = tw[r * e];
+    }
+}
+
+// v[r] *= W^(r*e) from the tw_fetch<R> entries (same products as twiddle<R, N>)
+template <int R>
+__device__ __forceinline__ void tw_apply(float2* v, const float2* w) {
+    if constexpr (R == 16) {
+        const float2 w1 = w[0], w2 = w[1], w3 = w[2], w4 = w[3], w8 = w[4], w12 = w[5];
+        v[1] = cmul(v[1], w1);
+        v[2] = cmul(v[2], w2);
+        v[3] = cmul(v[3], w3);
+        v[4] = cmul(v[4], w4);
+        v[5] = cmul(v[5], cmul(w4, w1));
+        v[6] = cmul(v[6], cmul(w4, w2));
+        v[7] = cmul(v[7], cmul(w4, w3));
+        v[8] = cmul(v[8], w8);
+        v[9] = cmul(v[9], cmul(w8, w1));
+        v[10] = cmul(v[10], cmul(w8, w2));
+        v[11] = cmul(v[11], cmul(w8, w3));
+        v[12] = cmul(v[12], w12);
+        v[13] = cmul(v[13], cmul(w12, w1));
+        v[14] = cmul(v[14], cmul(w12, w2));
+        v[15] = cmul(v[15], cmul(w12, w3));
+    } else if constexpr (R == 8) {
+        const float2 w1 = w[0], w2 = w[1], w3 = w[2], w4 = w[3];
+        v[1] = cmul(v[1], w1);
+        v[2] = cmul(v[2], w2);
+        v[3] = cmul(v[3], w3);
+        v[4] = cmul(v[4], w4);
+        v[5] = cmul(v[5], cmul(w4, w1));
+        v[6] = cmul(v[6], cmul(w4, w2));
+        v[7] = cmul(v[7], cmul(w4, w3));
+    } else {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], w[r - 1]);
+    }
+}
+
+template <int N, int G, int Ns, int E, int WO, int NW>
+__device__ __forceinline__ void tw_preload(float2 (&w)[NW], int t, const float2* __restrict__ tw) {
+    if constexpr (Ns < N) {
+        constexpr int R = pick_radix_e(N / Ns, E);
+        constexpr int PER = E / R;
+        constexpr int L = tw_loads(R);
+        if constexpr (Ns > 1) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int k = (t + i * G) % Ns;
+                tw_fetch<R>(w + WO + i * L, k * (N / (Ns * R)), tw);
+            }
+        }
+        tw_preload<N, G, Ns * R, E, WO + (Ns > 1 ? PER * L : 0), NW>(w, t, tw);
+    }
+}
+
+// fft_reg with the twiddles of every pass already in registers (w from tw_preload)
+template <int N, int G, int Ns, int E, int WO, int NW>
+__device__ __forceinline__ void fft_reg_w(float2 (&u)[E], float2* buf, int t, const float2 (&w)[NW]) {
+    if constexpr (Ns < N) {
+        constexpr int R = pick_radix_e(N / Ns, E);
+        static_assert(R != 0, "no radix divides both the remaining length and E");
+        constexpr int NB = N / R;
+        constexpr int PER = E / R;
+        constexpr int L = tw_loads(R);
+        static_assert(NB == PER * G, "thread count and radix plan disagree");
+        if constexpr (Ns > 1) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int b = t + i * G;
+#pragma unroll
+                for (int r = 0; r < R; ++r) u[i + r * PER] = buf[slot<NB, R>(b, r)];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            float2 v[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = u[i + r * PER];
+            if constexpr (Ns > 1) tw_apply<R>(v, w + WO + i * L);
+            dft<R>(v);
+#pragma unroll
+            for (int r = 0; r < R; ++r) u[i + r * PER] = v[r];
+        }
+        if constexpr (Ns * R < N) {
+            __syncthreads();  // WAR: earlier readers of buf are done
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int j = t + i * G;
+                const int base = (j / Ns) * Ns * R + (j % Ns);
+#pragma unroll
+                for (int r = 0; r < R; ++r) buf[slot<Ns, R>(base, r)] = u[i + r * PER];
+            }
+            __syncthreads();  // RAW
+        }
+        fft_reg_w<N, G, Ns * R, E, WO + (Ns > 1 ? PER * L : 0), NW>(u, buf, t, w);
     }
 }
 

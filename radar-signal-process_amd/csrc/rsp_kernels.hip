@@ -214,10 +214,17 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
 }
 
 // One row's matched-filter segment (and optionally its FIR segment) by G threads.
+// G >= 64: a row spans whole waves, so the row index is wave-uniform (readfirstlane makes
+// that visible to the compiler) and the row's input/output spans are buffer resources in
+// SGPRs -- the zero padding beyond in_len, the out_len cut and invalid rows (num_records 0)
+// are the hardware range check, with no per-element branch.  G < 64 (N <= 512): rows share
+// a wave, so the accesses stay per-lane predicated.
 template <typename TIn, int N, int G>
 __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
                                        const PcMfArgs& a, int row, int t, float2* buf) {
     constexpr int E = N / G;
+    constexpr bool kUniform = G % 64 == 0;
+    if constexpr (kUniform) row = __builtin_amdgcn_readfirstlane(row);
 #ifdef RSP_STAMPS
     const bool stamp_on = (N == 4096) && blockIdx.x < kStampBlocks;
     const int stamp_blk = blockIdx.x;
@@ -226,7 +233,11 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     const bool valid = row < a.rows;
     const TIn* x = echo + (size_t)row * a.R;
     float2* y = out + (size_t)row * a.R_out;
+#ifndef RSP_AB_NOFIR
     if (a.do_fir) {
+#else
+    if (false) {
+#endif
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
                 for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) y[c] = make_float2(0.f, 0.f);
@@ -234,36 +245,56 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     }
     const int in_start = a.mf.in_start, in_len = a.mf.in_len;
     const int out_start = a.mf.out_start, out_len = a.mf.out_len;
-    const float2* __restrict__ H = a.mf.H;
     const float2* __restrict__ tw = a.mf.tw;
+    constexpr uint32_t ES = sizeof(TIn);
+    const auto hr = buf_rsrc(a.mf.H, (uint32_t)N * 8u);
     float2 u[E];
+    constexpr int NW = tw_regs<N, E>() > 0 ? tw_regs<N, E>() : 1;
+    float2 w[NW];
+    tw_preload<N, G, 1, E, 0, NW>(w, t, tw);
+    if constexpr (kUniform) {
+        const auto xr = buf_rsrc(x + in_start, valid ? (uint32_t)in_len * ES : 0u);
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        const int i = t + G * m;
+        for (int m = 0; m < E; ++m) {
 #ifdef RSP_AB_NOLOAD
-        u[m] = make_float2((float)(i + row), a.mf.scale);
+            u[m] = make_float2((float)(t + G * m + row), a.mf.scale);
 #else
-        u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
+            u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
 #endif
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int i = t + G * m;
+            u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
+        }
     }
 #ifdef RSP_STAMPS
     if (stamp_on) { float acc = 0.f; for (int m = 0; m < E; ++m) acc += u[m].x; asm volatile("" :: "v"(acc)); }
 #endif
     RSP_STAMP(1);
-    fft_reg<N, G, 1, E>(u, buf, t, tw);
+    fft_reg_w<N, G, 1, E, 0, NW>(u, buf, t, w);
     RSP_STAMP(2);
 #ifndef RSP_AB_NOH
+    {
+        float2 h[E];   // one batch of spectrum loads, then the multiply
 #pragma unroll
-    for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], H[t + G * m]);  // conj(X.*H), 1/N in H
+        for (int m = 0; m < E; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+#pragma unroll
+        for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], h[m]);   // conj(X.*H), 1/N in H
+    }
 #endif
     RSP_STAMP(3);
-    fft_reg<N, G, 1, E>(u, buf, t, tw);
+    fft_reg_w<N, G, 1, E, 0, NW>(u, buf, t, w);
     RSP_STAMP(4);
+    if constexpr (kUniform) {
+        const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
 #ifdef RSP_AB_NOSTORE
-    if (u[0].x == 12345.678f) {
-#else
-    if (valid) {
+        if (u[0].x == 12345.678f)
 #endif
+#pragma unroll
+        for (int m = 0; m < E; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+    } else if (valid) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int i = t + G * m;
@@ -303,6 +334,9 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_PC_WAVES) voi
             return;
         }
     }
+#ifdef RSP_AB_NOSEG1
+    if (N2 != 0) return;
+#endif
     constexpr int G = PcCfg<N1>::G;
     const int grp = threadIdx.x / G, t = threadIdx.x % G;
     const int b = (int)blockIdx.x - (N2 ? nblk2 : 0);

@@ -177,9 +177,10 @@ class Engine:
                                  C.c_void_p(out.data_ptr()), self._stream_handle(stream))
         capi.check(rc, self.ctx)
 
-    def profile(self, enable=True):
-        """Start (and reset) or stop per-kernel HIP-event timing inside librsp."""
-        capi.check(self.lib.rsp_profile(self.ctx, 1 if enable else 0), self.ctx)
+    def profile(self, enable=True, every=1):
+        """Start (and reset) or stop per-kernel HIP-event timing inside librsp; `every` = N
+        brackets every N-th launch only (sampled timing inside a throughput measurement)."""
+        capi.check(self.lib.rsp_profile(self.ctx, int(every) if enable else 0), self.ctx)
 
     def profile_read(self):
         """{kernel name: (total ms, launches)} since profile(True)."""

@@ -7,9 +7,11 @@ cd "$ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
-timeout -k 10 ${PYTEST_LIMIT:-900} python -m pytest tests -m gpu -q --timeout 300 -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
-if fatal $rc; then exit $rc; fi
+if [ "${SKIP_PYTEST:-0}" != "1" ]; then
+  timeout -k 10 ${PYTEST_LIMIT:-900} python -m pytest tests -m gpu -q --timeout 300 -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
+  if fatal $rc; then exit $rc; fi
+fi
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-seconds ${CPU_SECONDS:-5} ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
