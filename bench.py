@@ -31,7 +31,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=3, help=">= 1 (the first warmup step counts launches)")
     ap.add_argument("--preset", default="v2", choices=["v2", "dmx"])
     ap.add_argument("--P", type=int, default=128)
     ap.add_argument("--R", type=int, default=4096)
@@ -88,6 +88,7 @@ def pmc_traffic(tag):
 
 def main():
     args = parse()
+    args.warmup = max(args.warmup, 1)
     import torch
     import torch.distributed as dist
     from rsp import presets, shard, synth
@@ -120,8 +121,14 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
+    launches_per_step = None
+    for i in range(args.warmup):
+        if i == 0 and not args.no_profile:
+            eng.profile(True, every=1)      # count launches per step (chunks) once, untimed
         step()
+        if i == 0 and not args.no_profile:
+            launches_per_step = {k: n for k, (_, n) in eng.profile_read().items()}
+            eng.profile(False)
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
@@ -169,9 +176,10 @@ def main():
             ks = {}
             for name, (ms, n) in kernels.items():
                 avg_us = ms * 1e3 / n
-                ks[name] = {"avg_us": round(avg_us, 2), "launches": n, "total_ms": round(ms, 3)}
+                ks[name] = {"avg_us": round(avg_us, 2), "sampled_launches": n,
+                            "launches_per_step": launches_per_step.get(name)}
             dom = max(kernels, key=lambda k: kernels[k][0])
-            cpl = B * args.steps / kernels[dom][1]      # CPIs per launch (chunk)
+            cpl = B / launches_per_step[dom]           # CPIs per launch (chunk)
             avg_s = kernels[dom][0] / 1e3 / kernels[dom][1]
             ach = cpi_bytes * cpl / avg_s / 1e9
             roof.update({"kernel": dom, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
@@ -183,7 +191,8 @@ def main():
                 roof["traffic"] = int(kp["hbm_bytes_per_launch"] * scale)
                 roof["traffic_source"] = "profiles/pmc_%s.json" % tag
             roof["kernels"] = ks
-            roof["kernel_sum_ms_per_step"] = round(sum(v[0] for v in kernels.values()) / args.steps, 3)
+            roof["kernel_sum_ms_per_step"] = round(
+                sum(kernels[k][0] / kernels[k][1] * launches_per_step[k] for k in kernels), 3)
         else:
             roof.update({"kernel": "chain", "achieved": round(chain_gbps, 1),
                          "frac": round(chain_gbps / HBM_PEAK_GBPS, 4)})

@@ -45,6 +45,8 @@ struct rsp_ctx {
     std::vector<void*> owned;           // constant tables (freed at destroy)
     std::map<int, float2*> tw;          // twiddle tables by length
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
+    DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
+    DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
     // diagnostics (rsp_profile): HIP event pairs around each kernel launch
     struct Ev {
@@ -196,8 +198,8 @@ int rsp_destroy(rsp_ctx* ctx) {
     if (!ctx) return RSP_OK;
     hipSetDevice(ctx->device);
     for (void* p : ctx->owned) hipFree(p);
-    DevBuf* bufs[] = {&ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->st_in, &ctx->st_canon,
-                      &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t};
+    DevBuf* bufs[] = {&ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
+                      &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -309,6 +311,16 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
             int rc = upload(ctx, tf, &dt);
             if (rc) return bail(rc);
             d.taps_dev = dt;
+            d.ntaps4 = (d.ntaps + 3) & ~3;
+            std::vector<float2> t2((size_t)d.ntaps4, float2{0.f, 0.f});
+            for (int k = 0; k < d.ntaps; ++k) {
+                const float b = (float)(g.coef_re[k] * g.scale);
+                t2[k] = float2{b, b};
+            }
+            float2* dt2 = nullptr;
+            rc = upload(ctx, t2, &dt2);
+            if (rc) return bail(rc);
+            d.taps2_dev = dt2;
             int64_t sh = g.fir_shift % g.out_len;
             if (sh < 0) sh += g.out_len;
             d.fir_shift = (int)sh;
@@ -380,7 +392,7 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
                     a.zero_lo[z] = pc.zero_lo[z];
                     a.zero_hi[z] = pc.zero_hi[z];
                 }
-                if (!rsp::pc_mf_supported(a.mf.nfft, a.do_fir ? a.fir.in_len : 0)) ok = false;
+                if (!rsp::pc_mf_supported(a.mf.nfft, a.do_fir ? rsp::fir_stage_len(a.fir) : 0)) ok = false;
                 first = 0;
             } else if (!rsp::pc_mf_supported(a.mf.nfft, 0)) {
                 ok = false;
@@ -696,8 +708,15 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
     const size_t cells = (size_t)chunk * P * Ro;   // per chunk slot
     int rc = ensure(ctx, ctx->scratch_pc, (size_t)ns * cells * sizeof(float2));
     if (rc) return rc;
-    if (cfar && !d_flagV) {
-        rc = ensure(ctx, ctx->tmp_flagV, (size_t)ns * cells);
+    if (cfar) {
+        // fused range stage: per-lane hit lists, one region per MTD workgroup sized to its
+        // cells (no overflow, no global atomics), and per-workgroup counts
+        if (cells > 0xffffffffull) return fail(ctx, RSP_ERR_UNSUPPORTED, "chunk too large for 32-bit hit indices");
+        int nreg = 0, reg = 0;
+        rsp::mtd_regions((int)P, (int)Ro, (int)chunk, &nreg, &reg);
+        rc = ensure(ctx, ctx->hit_list, (size_t)ns * nreg * reg * sizeof(uint32_t));
+        if (rc) return rc;
+        rc = ensure(ctx, ctx->hit_ctr, (size_t)ns * nreg * sizeof(uint32_t));
         if (rc) return rc;
     }
     if (!d_rdm) {
@@ -725,14 +744,25 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
         hipStream_t ls = lanes[lane];
         const char* ein = (const char*)d_echo + (size_t)c0 * P * R * esz;
         float* rdm = d_rdm ? d_rdm + (size_t)c0 * P * Ro : (float*)ctx->tmp_rdm.p + lane * cells;
-        uint8_t* fv = nullptr;
-        if (cfar) fv = d_flagV ? d_flagV + (size_t)c0 * P * Ro : (uint8_t*)ctx->tmp_flagV.p + lane * cells;
+        uint8_t* fv = (cfar && d_flagV) ? d_flagV + (size_t)c0 * P * Ro : nullptr;
         float2* pcs = (float2*)ctx->scratch_pc.p + lane * cells;
         HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * P, ls));
-        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, ls); }));
+        int nreg = 0, reg = 0;
         if (cfar) {
-            uint8_t* fl = d_flag + (size_t)c0 * P * Ro;
-            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] { return rsp::launch_cfar_r(rdm, fv, fl, (int)n, cr, ls); }));
+            rsp::mtd_regions((int)P, (int)Ro, (int)chunk, &nreg, &reg);
+            m.flag = d_flag + (size_t)c0 * P * Ro;
+            m.rflag = cr.rflag;
+            m.hits = (uint32_t*)ctx->hit_list.p + (size_t)lane * nreg * reg;
+            m.hit_count = (uint32_t*)ctx->hit_ctr.p + (size_t)lane * nreg;
+            rsp::mtd_regions((int)P, (int)Ro, (int)n, &nreg, &reg);   // this chunk's workgroups
+        }
+        if (cfar && cr.rflag)   // background of the flag plane; the range stage writes the 1s
+            HIP_TRY(ctx, hipMemsetAsync(m.flag, 0, (size_t)n * P * Ro, ls));
+        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, ls); }));
+        if (cfar && cr.rflag) {
+            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] {
+                return rsp::launch_cfar_hits(rdm, m.flag, m.hits, m.hit_count, nreg, reg, cr, ls);
+            }));
         }
     }
     for (int i = 1; i < ns; ++i) {

@@ -22,6 +22,8 @@ struct SegDev {
     const float2* H;   // MF: conj(FFT_nfft(scale*replica)) / nfft
     const float2* tw;  // MF: W_nfft^e table, e < nfft
     const float* taps_dev;  // FIR taps in device memory (no dynamic kernarg indexing)
+    int ntaps4;             // ntaps rounded up to a multiple of 4
+    const float2* taps2_dev;  // (scale*b_k, scale*b_k), zero-padded to ntaps4: one packed fma per tap
     float taps[RSP_MAX_FIR_TAPS];
 };
 
@@ -66,6 +68,14 @@ struct MtdArgs {
     const float* win;    // slow-time window, P entries
     const float2* tw;    // W_P^e table
     CfarVArgs cv;
+    // Fused range-CFAR front end (cv.enabled): the MTD kernel writes the final flag plane's
+    // background -- flagV itself when rflag == 0, zeros otherwise -- and appends every
+    // in-band Doppler hit (linear cell index within the launch) to `hits`; cfar_hits_kernel
+    // then sets the re-localised range detections.  flagV is written only when requested.
+    uint8_t* flag;
+    int rflag;
+    uint32_t* hits;        // workgroup b owns hits[b*W*P, (b+1)*W*P) (its own cells: no overflow)
+    uint32_t* hit_count;   // hit_count[b] = entries of workgroup b (b = blockIdx.y*gridDim.x + blockIdx.x)
 };
 
 // Range-dimension CFAR at the Doppler hits (executeCFAR.m:35-89).
@@ -87,7 +97,10 @@ size_t pc_lds_bytes(int max_nfft);
 
 hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, const PcArgs& a,
                      size_t lds_bytes, hipStream_t s);
-bool pc_mf_supported(int nfft, int fir_in_len);
+// float2 slots the FIR stages in the row's LDS slot: ntaps4-1 leading zeros, the segment,
+// and the 4-output block's read-ahead
+inline int fir_stage_len(const SegDev& g) { return g.ntaps4 - 1 + g.out_len + 4; }
+bool pc_mf_supported(int nfft, int fir_stage_len);
 bool pc_pair_supported(int nfft1, int nfft2);
 // a2 == nullptr: one segment; otherwise both segments (a1.mf.nfft, a2->mf.nfft) in one launch
 hipError_t launch_pc_mf(const void* echo, int dtype, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
@@ -97,6 +110,12 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
 // Doppler CFAR straight from an RDM ([ncpi][V][R] fp32) for rsp_cfar.
 hipError_t launch_cfar_v(const float* rdm, uint8_t* flagV, int ncpi, int V, int R,
                          const CfarVArgs& a, hipStream_t s);
+// Range CFAR + re-localisation at the Doppler hits listed by the MTD kernel (scatter form of
+// executeCFAR.m:45-84).  `zero_slot` (if non-null) is reset for a later launch.
+hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
+                            int nregions, int region, const CfarRArgs& a, hipStream_t s);
+// MTD workgroups per launch and cells per workgroup (hit-list regions)
+void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region);
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
                          const CfarRArgs& a, hipStream_t s);
 // dtype/layout conversion of a host-API input into [batch][P][R] complex float32.

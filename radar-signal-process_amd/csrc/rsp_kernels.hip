@@ -189,26 +189,53 @@ struct PcCfg {
     static constexpr size_t lds = (size_t)RPB * SLOT * sizeof(float2);
 };
 
+// FIR segment of one row (fun_lss_pulse_compression.m:38-51): z = filter(b, 1, x_A) * scale
+// (causal, zero initial state), out[n] = z[(n + shift) mod len].  The segment is staged in
+// the row's LDS slot behind ntaps4-1 zeros, so z[m] = sum_k b_k s[kp + m - k] needs no
+// bounds test.  A thread produces 4 consecutive z and walks the taps 4 at a time: 7 LDS
+// reads and 16 packed fmas per step (taps pre-scaled and duplicated as (b, b), so a wave-
+// uniform tap multiplies both I and Q in one v_pk_fma_f32).
+__device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
+    return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
+}
+
 template <typename TIn, int G>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t) {
-    // stage the segment's input, then y[n] = scale * sum_k taps[k] x[m-k], m = (n+shift) mod len
     float2* s2 = reinterpret_cast<float2*>(stage);
-    for (int i = t; i < g.in_len; i += G) s2[i] = valid ? ld_c(x + g.in_start + i) : make_float2(0.f, 0.f);
+    const int kp = g.ntaps4 - 1;
+    const int len = g.out_len;
+    for (int i = t; i < kp + len + 4; i += G) {
+        const int j = i - kp;
+        s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+    }
     __syncthreads();
-    for (int n = t; n < g.out_len; n += G) {
-        int m = n + g.fir_shift;
-        if (m >= g.out_len) m -= g.out_len;
-        float ar = 0.f, ai = 0.f;
-        const int kmax = m + 1 < g.ntaps ? m + 1 : g.ntaps;
-        const float* __restrict__ taps = g.taps_dev;
-        for (int k = 0; k < kmax; ++k) {
-            const float2 v = s2[m - k];
-            const float b = taps[k];
-            ar = fmaf(b, v.x, ar);
-            ai = fmaf(b, v.y, ai);
+    const float2* __restrict__ taps = g.taps2_dev;
+    for (int m0 = 4 * t; m0 < len; m0 += 4 * G) {
+        float2 acc[4] = {};
+        const float2* p = s2 + kp + m0;     // p[i] = x[m0 + i]
+        for (int k = 0; k < g.ntaps4; k += 4) {
+            float2 w[7];                     // w[q] = x[m0 + q - 3 - k]
+#pragma unroll
+            for (int q = 0; q < 7; ++q) w[q] = p[q - 3 - k];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const float2 b = taps[k + kk];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i - kk + 3], b, acc[i]);
+            }
         }
-        if (valid) y[g.out_start + n] = make_float2(ar * g.scale, ai * g.scale);
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + i;
+                if (m < len) {
+                    int n = m - g.fir_shift;
+                    if (n < 0) n += len;
+                    y[g.out_start + n] = acc[i];
+                }
+            }
+        }
     }
     __syncthreads();
 }
@@ -276,12 +303,16 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     fft_reg_w<N, G, 1, E, 0, NW>(u, buf, t, w);
     RSP_STAMP(2);
 #ifndef RSP_AB_NOH
-    {
-        float2 h[E];   // one batch of spectrum loads, then the multiply
+#ifndef RSP_HB
+#define RSP_HB 8
+#endif
 #pragma unroll
-        for (int m = 0; m < E; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+    for (int m0 = 0; m0 < E; m0 += RSP_HB) {
+        float2 h[RSP_HB];   // batches of spectrum loads, then the multiply
 #pragma unroll
-        for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], h[m]);   // conj(X.*H), 1/N in H
+        for (int m = 0; m < RSP_HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * (m0 + m)) * 8u);
+#pragma unroll
+        for (int m = 0; m < RSP_HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
     }
 #endif
     RSP_STAMP(3);
@@ -343,11 +374,126 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_PC_WAVES) voi
     pc_row<TIn, N1, G>(echo, out, a1, b * PC::RPB1 + grp, t, lds + grp * PcCfg<N1>::SLOT);
 }
 
-bool pc_mf_supported(int nfft, int fir_in_len) {
+// ---------------------------------------------------------------- persistent pair kernel
+// One long-segment row is G = T threads; the grid is sized to the resident block count and
+// each block walks the items blockIdx.x, +gridDim.x, ...: items [0, n2) are long-segment rows,
+// [n2, nitems) groups of RPB1 short-segment rows (FIR + MF).  Per long row: the row's
+// twiddles and its slice of H stay in registers for the whole launch, the next row's input
+// is loaded while this row runs the spectrum multiply and the inverse FFT, and the block
+// moves on without waiting for its stores -- the load, H-table and store-drain latencies
+// that bound the one-row-per-block kernel overlap with the FFT work.
+template <typename TIn, int N, int G>
+__device__ __forceinline__ void mf_load(float2 (&u)[N / G], const TIn* __restrict__ echo, const PcMfArgs& a,
+                                        int row, bool valid, int t) {
+    constexpr uint32_t ES = sizeof(TIn);
+    const auto xr = buf_rsrc(echo + (size_t)row * a.R + a.mf.in_start, valid ? (uint32_t)a.mf.in_len * ES : 0u);
+#pragma unroll
+    for (int m = 0; m < N / G; ++m)
+        u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
+}
+
+template <int N, int G>
+__device__ __forceinline__ void mf_store(const float2 (&u)[N / G], float2* __restrict__ out, const PcMfArgs& a,
+                                         int row, int t) {
+    const auto yr = buf_rsrc(out + (size_t)row * a.R_out + a.mf.out_start, (uint32_t)a.mf.out_len * 8u);
+#pragma unroll
+    for (int m = 0; m < N / G; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+}
+
+#ifndef RSP_PERSIST_WAVES
+#define RSP_PERSIST_WAVES 2
+#endif
+template <typename TIn, int N1, int N2>
+__global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_persist_kernel(
+    const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int n2, int nitems) {
+    using PC = PairCfg<N1, N2>;
+    static_assert(PcCfg<N2>::G == PC::T, "one long-segment row per workgroup");
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    int item = blockIdx.x;
+    if (item < n2) {
+        constexpr int G = PcCfg<N2>::G, E = N2 / G;
+        constexpr int NW = tw_regs<N2, E>() > 0 ? tw_regs<N2, E>() : 1;
+        const int t = threadIdx.x;
+        float2 w[NW];
+        tw_preload<N2, G, 1, E, 0, NW>(w, t, a2.mf.tw);
+        float2 h[E];
+        const auto hr = buf_rsrc(a2.mf.H, (uint32_t)N2 * 8u);
+#pragma unroll
+        for (int m = 0; m < E; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+        float2 u[E];
+        mf_load<TIn, N2, G>(u, echo, a2, item, true, t);
+        // settle the entry loads here, so the loop header carries no pending load (a merged
+        // wait state would put a vmcnt(0) -- a store drain -- at the top of every iteration)
+#pragma unroll
+        for (int m = 0; m < E; ++m) asm volatile("" ::"v"(u[m]), "v"(h[m]));
+        while (item < n2) {
+            const int next = item + (int)gridDim.x;
+            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, w);
+            float2 nx[E];   // next row in flight during the multiply + inverse FFT
+            mf_load<TIn, N2, G>(nx, echo, a2, next < n2 ? next : item, next < n2, t);
+#pragma unroll
+            for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], h[m]);   // conj(X.*H), 1/N in H
+            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, w);
+            // Consume the prefetch before the stores are issued: loads and stores share vmcnt
+            // on gfx9, so a wait placed after the stores (at the next row's first use) would
+            // also drain them.  Here the wait is for loads issued a multiply + IFFT ago.
+#pragma unroll
+            for (int m = 0; m < E; ++m) asm volatile("" ::"v"(nx[m]));
+            mf_store<N2, G>(u, out, a2, item, t);
+#pragma unroll
+            for (int m = 0; m < E; ++m) u[m] = nx[m];
+            item = next;
+        }
+    }
+#ifdef RSP_AB_NOSEG1
+    return;
+#endif
+    constexpr int G1 = PcCfg<N1>::G;
+    const int grp = threadIdx.x / G1, t1 = threadIdx.x % G1;
+    for (; item < nitems; item += (int)gridDim.x) {
+        __syncthreads();   // the previous item's last LDS reads are done
+        pc_row<TIn, N1, G1>(echo, out, a1, (item - n2) * PC::RPB1 + grp, t1, lds + grp * PcCfg<N1>::SLOT);
+    }
+}
+
+static int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+    }
+    return cus;
+}
+
+template <typename TIn, int N1, int N2>
+static hipError_t launch_pc_persist(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs& a2,
+                                    hipStream_t s) {
+    using PC = PairCfg<N1, N2>;
+    static int resident = 0;
+    if (!resident) {
+        hipError_t e = hipFuncSetAttribute((const void*)pc_persist_kernel<TIn, N1, N2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)PC::lds);
+        if (e != hipSuccess) return e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_persist_kernel<TIn, N1, N2>,
+                                                         PC::T, PC::lds);
+        if (e != hipSuccess) return e;
+        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
+    }
+    const int n2 = a1.rows;                                  // one item per long-segment row
+    const int nitems = n2 + (a1.rows + PC::RPB1 - 1) / PC::RPB1;
+    const int grid = nitems < resident ? nitems : resident;
+    hipLaunchKernelGGL((pc_persist_kernel<TIn, N1, N2>), dim3((unsigned)grid), dim3(PC::T), PC::lds, s, echo, out,
+                       a1, a2, n2, nitems);
+    return hipGetLastError();
+}
+
+bool pc_mf_supported(int nfft, int fir_stage_len) {
     switch (nfft) {
         case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: case 8192:
         case 16384:
-            return fir_in_len <= padded_len(nfft);   // the FIR stages its input in the row's slot
+            return fir_stage_len <= padded_len(nfft);   // the FIR stages its input in the row's slot
         default:
             return false;
     }
@@ -373,15 +519,23 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     return hipGetLastError();
 }
 
+#ifndef RSP_PC_PERSIST
+#define RSP_PC_PERSIST 1
+#endif
 #define RSP_PAIR(n1, n2) \
     if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s)
+#define RSP_PAIR_PERSIST(n1, n2)                                                              \
+    if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) {                                        \
+        if (RSP_PC_PERSIST) return launch_pc_persist<TIn, n1, n2>(echo, out, a1, *a2, s);     \
+        return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s);                             \
+    }
 
 template <typename TIn>
 static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
                                  hipStream_t s) {
     // fused pairs of the built-in presets (v2 at 1024..16384 range bins, legacy)
     RSP_PAIR(1024, 1024);
-    RSP_PAIR(1024, 4096);
+    RSP_PAIR_PERSIST(1024, 4096);
     RSP_PAIR(1024, 8192);
     RSP_PAIR(1024, 16384);
     RSP_PAIR(512, 1024);
@@ -400,6 +554,7 @@ static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a
     }
 }
 #undef RSP_PAIR
+#undef RSP_PAIR_PERSIST
 
 bool pc_pair_supported(int n1, int n2) {
     return (n1 == 1024 && (n2 == 1024 || n2 == 4096 || n2 == 8192 || n2 == 16384)) || (n1 == 512 && n2 == 1024);
@@ -459,16 +614,22 @@ __device__ __forceinline__ void doppler_sums(const float* mag, float* sums, int 
     }
 }
 
+__device__ __forceinline__ uint8_t doppler_test(const float* mag, const float* sums, const CfarVArgs& cv,
+                                                bool col_on, int v) {
+    uint8_t f = 0;
+    if (col_on && v >= cv.lo && v < cv.hi) {
+        const int l1 = v - cv.save - cv.ref, r1 = v + cv.save + 1;
+        const bool lok = l1 >= cv.lo, rok = r1 + cv.ref <= cv.hi;
+        f = cfar_test(mag[v], lok ? sums[l1] : 0.f, rok ? sums[r1] : 0.f, lok, rok, cv.method, cv.Tr);
+    }
+    return f;
+}
+
 __device__ __forceinline__ void doppler_flags(const float* mag, const float* sums, const CfarVArgs& cv, bool col_on,
                                               int v0, int v1, uint8_t* __restrict__ out, size_t R, bool rv) {
     out += (size_t)v0 * R;
     for (int v = v0; v < v1; ++v) {
-        uint8_t f = 0;
-        if (col_on && v >= cv.lo && v < cv.hi) {
-            const int l1 = v - cv.save - cv.ref, r1 = v + cv.save + 1;
-            const bool lok = l1 >= cv.lo, rok = r1 + cv.ref <= cv.hi;
-            f = cfar_test(mag[v], lok ? sums[l1] : 0.f, rok ? sums[r1] : 0.f, lok, rok, cv.method, cv.Tr);
-        }
+        const uint8_t f = doppler_test(mag, sums, cv, col_on, v);
         if (rv) *out = f;
         out += R;
     }
@@ -499,10 +660,46 @@ struct MtdCfg {
 // look-ahead rows is read from LDS once; its E window sums are direct left-to-right adds
 // (the order mean() uses) and go to a padded sums column, so the left/right window lookups
 // of every row are unclamped LDS reads with immediate offsets.
+// Per-row outputs of the Doppler CFAR at cell (v, r) of launch CPI `cpi`: flagV (if requested),
+// the flag plane's background (flagV when the range stage is off, else 0) and, for a hit
+// with the range stage on, an entry in the hit list (one atomic per wave and row).
+struct DopplerOut {
+    __amdgpu_buffer_rsrc_t fv, fl;   // flagV / flag planes of this CPI (num_records 0 if absent)
+    uint32_t vo;                     // this lane's cell offset (row v0, column r) or kOob
+    uint32_t R;
+    uint32_t* hits;                  // this workgroup's region of the hit list
+    uint32_t* lds_count;             // workgroup hit counter (LDS)
+    uint32_t cell0;                  // linear index of (v0, r) within the launch
+    bool want_fv, fused, rflag;
+};
+
+__device__ __forceinline__ void doppler_emit(const DopplerOut& o, bool hit, int i) {
+    const uint32_t so = (uint32_t)i * o.R;
+    if (o.want_fv) buf_st_u8(hit ? 1 : 0, o.fv, o.vo, so);
+    if (o.fused) {
+        if (!o.rflag) buf_st_u8(hit ? 1 : 0, o.fl, o.vo, so);   // flag = flagV (executeCFAR.m:91)
+        else {   // flag plane pre-zeroed by the host; the range stage sets the detections
+            const uint64_t bal = __ballot(hit);
+            if (bal) {   // rare: hits are sparse
+                const int lane = __lane_id();
+                const int leader = __builtin_ctzll(bal);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(o.lds_count, (uint32_t)__popcll(bal));
+                base = __shfl(base, leader);
+                if (hit) o.hits[base + __popcll(bal & ((1ull << lane) - 1))] = o.cell0 + so;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void doppler_flags(const float* mag, const float* sums, const CfarVArgs& cv, bool col_on,
+                                              int v0, int v1, const DopplerOut& o) {
+    for (int v = v0; v < v1; ++v) doppler_emit(o, doppler_test(mag, sums, cv, col_on, v) != 0, v - v0);
+}
+
 template <int P, int REF, bool GO>
 __device__ __forceinline__ void doppler_rows_fixed(const float* m, const float* sums, const CfarVArgs& cv,
-                                                   bool col_on, int v0, __amdgpu_buffer_rsrc_t out,
-                                                   uint32_t vo, uint32_t R) {
+                                                   bool col_on, int v0, const DopplerOut& o) {
     constexpr int E = MtdCfg<P>::E;
     const int kl = cv.lo + cv.save + REF - v0;     // row v0+i has a left window iff i >= kl
     const int kr = cv.hi - cv.save - 1 - REF - v0; // ... and a right window iff i <= kr
@@ -517,7 +714,7 @@ __device__ __forceinline__ void doppler_rows_fixed(const float* m, const float* 
         // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
         const float th = (GO ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
         const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
-        buf_st_u8(hit ? 1 : 0, out, vo, (uint32_t)i * R);
+        doppler_emit(o, hit, i);
     }
 }
 
@@ -528,8 +725,7 @@ __device__ __forceinline__ void doppler_rows_fixed(const float* m, const float* 
 // window lookups are unclamped LDS reads with immediate offsets.
 template <int P, int REF>
 __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums, const CfarVArgs& cv,
-                                                   bool col_on, int v0, __amdgpu_buffer_rsrc_t out,
-                                                   uint32_t vo, uint32_t R) {
+                                                   bool col_on, int v0, const DopplerOut& o) {
     constexpr int E = MtdCfg<P>::E;
     float m[E + REF - 1];
 #pragma unroll
@@ -542,8 +738,8 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums
         sums[v0 + i] = acc;
     }
     __syncthreads();
-    if (cv.method == 0) doppler_rows_fixed<P, REF, true>(m, sums, cv, col_on, v0, out, vo, R);
-    else doppler_rows_fixed<P, REF, false>(m, sums, cv, col_on, v0, out, vo, R);
+    if (cv.method == 0) doppler_rows_fixed<P, REF, true>(m, sums, cv, col_on, v0, o);
+    else doppler_rows_fixed<P, REF, false>(m, sums, cv, col_on, v0, o);
 }
 
 // MTD: one workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the
@@ -560,6 +756,8 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     using C = MtdCfg<P>;
     constexpr int G = C::G, E = C::E, W = C::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_hits;
+    if (threadIdx.x == 0) s_hits = 0u;   // published by the FFT's barriers
     const int c = threadIdx.x % W, g = threadIdx.x / W;
     const size_t cpi = blockIdx.y;
     const uint32_t R = (uint32_t)a.R_out;
@@ -605,15 +803,29 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     __syncthreads();
     const int v0 = g * E;   // this thread's run of Doppler rows
     const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
+    DopplerOut o;
+    o.want_fv = flagV != nullptr;
+    o.fused = a.flag != nullptr;
+    o.rflag = a.rflag != 0;
+    o.fv = buf_rsrc(o.want_fv ? flagV + cpi * plane : nullptr, o.want_fv ? plane : 0u);
+    o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
+    o.vo = rv ? (uint32_t)v0 * R + (uint32_t)r : kOob;
+    o.R = R;
+    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+    o.hits = a.hits ? a.hits + (size_t)wg * (W * P) : nullptr;
+    o.lds_count = &s_hits;
+    o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
+    float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
     if constexpr (REF > 0) {
-        float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
-        const auto fo = buf_rsrc(flagV + cpi * plane, plane);
-        doppler_cfar_fixed<P, REF>(mag, sums, a.cv, col_on, v0, fo, rv ? (uint32_t)v0 * R + r : kOob, R);
+        doppler_cfar_fixed<P, REF>(mag, sums, a.cv, col_on, v0, o);
     } else {
-        float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
         doppler_sums(mag, sums, P, a.cv.ref, v0, v0 + E);
         __syncthreads();
-        doppler_flags(mag, sums, a.cv, col_on, v0, v0 + E, flagV + cpi * (size_t)P * R + r, R, rv);
+        doppler_flags(mag, sums, a.cv, col_on, v0, v0 + E, o);
+    }
+    if (o.fused && o.rflag) {
+        __syncthreads();
+        if (threadIdx.x == 0) a.hit_count[wg] = s_hits;
     }
 }
 
@@ -644,6 +856,25 @@ static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int
     if ((uint64_t)P * a.R_out * 8 >= (uint64_t)kOob) return hipErrorInvalidValue;
     if (a.cv.enabled && a.cv.ref == 5) return launch_mtd_pr<P, 5>(pc, rdm, flagV, ncpi, a, s);
     return launch_mtd_pr<P, 0>(pc, rdm, flagV, ncpi, a, s);
+}
+
+template <int P>
+static void mtd_regions_p(int R_out, int ncpi, int* nregions, int* region) {
+    using C = MtdCfg<P>;
+    *nregions = ((R_out + C::W - 1) / C::W) * ncpi;
+    *region = C::W * P;
+}
+
+void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region) {
+    *nregions = 0;
+    *region = 0;
+    switch (P) {
+#define RSP_MR(p) case p: mtd_regions_p<p>(R_out, ncpi, nregions, region); break;
+        RSP_MR(16) RSP_MR(32) RSP_MR(64) RSP_MR(128) RSP_MR(256) RSP_MR(512) RSP_MR(1024)
+        RSP_MR(48) RSP_MR(96) RSP_MR(192) RSP_MR(384) RSP_MR(768) RSP_MR(1536)
+#undef RSP_MR
+        default: break;
+    }
 }
 
 bool mtd_size_supported(int P) {
@@ -849,34 +1080,14 @@ __global__ __launch_bounds__(kBlock) void cfar_r_generic_kernel(const float* __r
 // forms the 16 window sums it needs in MATLAB's summation order, evaluates the range test
 // at c0-2 .. c0+5 and resolves the four outputs as in cfar_r_generic_kernel.  Cells whose
 // windows cross a segment edge take the segment-aware branch.
+// Range CFAR + re-localisation for the 4 cells c0..c0+3 of one RDM row (slow path: some
+// Doppler hit in c0-1..c0+4).  fa/fb/fc: flagV words of cells c0-4.., c0.., c0+4.. .
 template <int REF, int SAVE>
-__global__ __launch_bounds__(kBlock) void cfar_r_kernel(const float* __restrict__ rdm,
-                                                        const uint8_t* __restrict__ flagV,
-                                                        uint8_t* __restrict__ flag, CfarRArgs a, int groups) {
+__device__ __forceinline__ uint32_t cfar4(const float* __restrict__ xr, uint32_t fa, uint32_t fb, uint32_t fc,
+                                          int c0, int R, bool zrow, const CfarRArgs& a) {
     constexpr int H = SAVE + REF + 2;          // farthest x offset a result depends on
     constexpr int B = (H + 3) & ~3;            // aligned halo
     constexpr int NX = 4 + 2 * B;              // x values held per thread
-    const int R = a.R;
-    const int v = blockIdx.x / groups;
-    const int c0 = ((blockIdx.x % groups) * kBlock + threadIdx.x) * 4;
-    if (c0 >= R) return;
-    const size_t cpi = blockIdx.y;
-    const size_t rowoff = (cpi * (size_t)a.V + v) * (size_t)R;
-    uint32_t* out = reinterpret_cast<uint32_t*>(flag + rowoff + c0);
-    if (v < a.lo || v >= a.hi) {
-        *out = 0u;
-        return;
-    }
-    const uint32_t* fvw = reinterpret_cast<const uint32_t*>(flagV + rowoff);
-    const uint32_t fa = c0 >= 4 ? fvw[c0 / 4 - 1] : 0u;
-    const uint32_t fb = fvw[c0 / 4];
-    const uint32_t fc = c0 + 4 < R ? fvw[c0 / 4 + 1] : 0u;
-    if ((fa >> 24) == 0 && fb == 0 && (fc & 0xff) == 0) {   // no Doppler hit can reach these cells
-        *out = 0u;
-        return;
-    }
-    const bool zrow = (v >= a.cz_lo && v < a.cz_hi);
-    const float* xr = rdm + rowoff;
     float x[NX];   // x[k] = row[c0 - B + k]
 #pragma unroll
     for (int k = 0; k < NX; k += 4) {
@@ -935,7 +1146,149 @@ __global__ __launch_bounds__(kBlock) void cfar_r_kernel(const float* __restrict_
         }
         if (f) word |= 1u << (8 * j);
     }
-    *out = word;
+    return word;
+}
+
+template <int REF, int SAVE>
+__global__ __launch_bounds__(kBlock) void cfar_r_kernel(const float* __restrict__ rdm,
+                                                        const uint8_t* __restrict__ flagV,
+                                                        uint8_t* __restrict__ flag, CfarRArgs a, int groups) {
+    const int R = a.R;
+    const int v = blockIdx.x / groups;
+    const int c0 = ((blockIdx.x % groups) * kBlock + threadIdx.x) * 4;
+    if (c0 >= R) return;
+    const size_t cpi = blockIdx.y;
+    const size_t rowoff = (cpi * (size_t)a.V + v) * (size_t)R;
+    uint32_t* out = reinterpret_cast<uint32_t*>(flag + rowoff + c0);
+    if (v < a.lo || v >= a.hi) {
+        *out = 0u;
+        return;
+    }
+    const uint32_t* fvw = reinterpret_cast<const uint32_t*>(flagV + rowoff);
+    const uint32_t fa = c0 >= 4 ? fvw[c0 / 4 - 1] : 0u;
+    const uint32_t fb = fvw[c0 / 4];
+    const uint32_t fc = c0 + 4 < R ? fvw[c0 / 4 + 1] : 0u;
+    if ((fa >> 24) == 0 && fb == 0 && (fc & 0xff) == 0) {   // no Doppler hit can reach these cells
+        *out = 0u;
+        return;
+    }
+    *out = cfar4<REF, SAVE>(rdm + rowoff, fa, fb, fc, c0, R, v >= a.cz_lo && v < a.cz_hi, a);
+}
+
+// 16 cells per thread (R % 16 == 0): one 16-B flagV load, the neighbouring groups' edge
+// words from the adjacent lanes, one 16-B flag store; the 4-cell slow path runs only for
+// groups with a Doppler hit within reach.  Hits are sparse, so this is the streaming pass
+// over flagV -> flag at a quarter of the waves and memory instructions of cfar_r_kernel.
+template <int REF, int SAVE>
+__global__ __launch_bounds__(kBlock) void cfar_r16_kernel(const float* __restrict__ rdm,
+                                                          const uint8_t* __restrict__ flagV,
+                                                          uint8_t* __restrict__ flag, CfarRArgs a, int groups) {
+    const int R = a.R;
+    const int v = blockIdx.x / groups;
+    const int c0 = ((blockIdx.x % groups) * kBlock + threadIdx.x) * 16;
+    const bool in = c0 < R;
+    const size_t cpi = blockIdx.y;
+    const size_t rowoff = (cpi * (size_t)a.V + v) * (size_t)R;
+    const bool row_on = v >= a.lo && v < a.hi;
+    if (!in) return;
+    // this group's 16 flags and the edge words of the neighbouring groups, all in one round
+    // trip (the neighbours' words sit in the cache lines the adjacent lanes fetch anyway)
+    uint4 f = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t left = 0u, right = 0u;
+    if (row_on) {
+        const uint8_t* fr = flagV + rowoff;
+        f = *reinterpret_cast<const uint4*>(fr + c0);
+        if (c0 >= 16) left = *reinterpret_cast<const uint32_t*>(fr + c0 - 4);
+        if (c0 + 16 < R) right = *reinterpret_cast<const uint32_t*>(fr + c0 + 16);
+    }
+    uint4 o = make_uint4(0u, 0u, 0u, 0u);
+    if (row_on && ((left >> 24) | f.x | f.y | f.z | f.w | (right & 0xff)) != 0) {
+        const float* xr = rdm + rowoff;
+        const bool zrow = v >= a.cz_lo && v < a.cz_hi;
+        const uint32_t w[6] = {left, f.x, f.y, f.z, f.w, right};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const uint32_t fa = w[g], fb = w[g + 1], fc = w[g + 2];
+            uint32_t r = 0u;
+            if ((fa >> 24) != 0 || fb != 0 || (fc & 0xff) != 0) r = cfar4<REF, SAVE>(xr, fa, fb, fc, c0 + 4 * g, R, zrow, a);
+            (g == 0 ? o.x : g == 1 ? o.y : g == 2 ? o.z : o.w) = r;
+        }
+    }
+    *reinterpret_cast<uint4*>(flag + rowoff + c0) = o;
+}
+
+// Scatter form of the range stage: one thread per Doppler hit (v, r) of the MTD kernel's
+// list.  Candidates q in {r-1, r, r+1} within r's column segment take the range CFAR test
+// (Function_CFAR1D_sub_fixCells.m:34-58, one-sided fallback at segment edges); the first
+// maximum among passing candidates gets flag 1 (executeCFAR.m:64-84).  Several hits may
+// pick one cell; the writes are all 1.  Window sums are direct left-to-right adds.
+constexpr int kHitWaves = 4;   // regions per workgroup (one wave each)
+
+// REF/SAVE > 0: compile-time windows (every load of a hit's window issues at once);
+// 0: the runtime ref/save of CfarRArgs.
+template <int REF, int SAVE>
+__global__ __launch_bounds__(64 * kHitWaves) void cfar_hits_kernel(const float* __restrict__ rdm,
+                                                                   uint8_t* __restrict__ flag,
+                                                                   const uint32_t* __restrict__ hits,
+                                                                   const uint32_t* __restrict__ counts, int nregions,
+                                                                   int region, CfarRArgs a) {
+    const int rg = blockIdx.x * kHitWaves + (int)(threadIdx.x >> 6);
+    if (rg >= nregions) return;
+    const uint32_t n = counts[rg];
+    const uint32_t* list = hits + (size_t)rg * region;
+    const int R = a.R, V = a.V;
+    const int ref = REF > 0 ? REF : a.ref, save = REF > 0 ? SAVE : a.save;
+    for (uint32_t i = threadIdx.x & 63; i < n; i += 64) {
+        const uint32_t idx = list[i];
+        const uint32_t row = idx / (uint32_t)R;        // cpi * V + v
+        const int r = (int)(idx - row * (uint32_t)R);
+        const int v = (int)(row % (uint32_t)V);
+        int slo, shi;
+        seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
+        if (shi <= slo) continue;
+        const bool zrow = v >= a.cz_lo && v < a.cz_hi;
+        const float* xr = rdm + (size_t)row * R;
+        auto X = [&](int c) { return (!zrow && c >= 0 && c < R) ? xr[c] : 0.f; };
+        int best = -1;
+        float bx = 0.f;
+#pragma unroll
+        for (int e = -1; e <= 1; ++e) {
+            const int q = r + e;
+            float sl = 0.f, sr = 0.f;
+            if constexpr (REF > 0) {
+#pragma unroll
+                for (int k = 0; k < REF; ++k) {
+                    sl += X(q - SAVE - REF + k);
+                    sr += X(q + SAVE + 1 + k);
+                }
+            } else {
+                for (int k = 0; k < ref; ++k) {
+                    sl += X(q - save - ref + k);
+                    sr += X(q + save + 1 + k);
+                }
+            }
+            const bool lok = q - save - ref >= slo, rok = q + save + ref < shi;
+            const float xq = X(q);
+            if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
+                best = q;
+                bx = xq;
+            }
+        }
+        if (best >= 0) flag[(size_t)row * R + best] = 1;
+    }
+}
+
+hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
+                            int nregions, int region, const CfarRArgs& a, hipStream_t s) {
+    if (nregions <= 0) return hipSuccess;
+    const int grid = (nregions + kHitWaves - 1) / kHitWaves;
+    if (a.ref == 5 && a.save == 7)   // the reference's parameters
+        hipLaunchKernelGGL((cfar_hits_kernel<5, 7>), dim3((unsigned)grid), dim3(64 * kHitWaves), 0, s, rdm, flag,
+                           hits, counts, nregions, region, a);
+    else
+        hipLaunchKernelGGL((cfar_hits_kernel<0, 0>), dim3((unsigned)grid), dim3(64 * kHitWaves), 0, s, rdm, flag,
+                           hits, counts, nregions, region, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
@@ -950,7 +1303,13 @@ hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, 
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    if (a.ref == 5 && a.save == 7 && a.rflag && (a.R & 3) == 0) {   // the reference's parameters
+    if (a.ref == 5 && a.save == 7 && a.rflag && (a.R & 15) == 0) {   // the reference's parameters
+        const int groups = (a.R / 16 + kBlock - 1) / kBlock;
+        dim3 grid((unsigned)(groups * a.V), (unsigned)ncpi), block(kBlock);
+        hipLaunchKernelGGL((cfar_r16_kernel<5, 7>), grid, block, 0, s, rdm, flagV, flag, a, groups);
+        return hipGetLastError();
+    }
+    if (a.ref == 5 && a.save == 7 && a.rflag && (a.R & 3) == 0) {
         const int groups = (a.R / 4 + kBlock - 1) / kBlock;
         dim3 grid((unsigned)(groups * a.V), (unsigned)ncpi), block(kBlock);
         hipLaunchKernelGGL((cfar_r_kernel<5, 7>), grid, block, 0, s, rdm, flagV, flag, a, groups);

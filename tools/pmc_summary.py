@@ -51,7 +51,11 @@ def main():
         for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
                   "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS",
                   "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
-                  "SQ_ACTIVE_INST_ANY", "TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE"):
+                  "SQ_ACTIVE_INST_ANY", "TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE",
+                  "SQ_LDS_IDX_ACTIVE", "SQ_LDS_DATA_FIFO_FULL", "SQ_LDS_CMD_FIFO_FULL", "SQ_INST_LEVEL_LDS",
+                  "SQ_LEVEL_WAVES", "SQ_BUSY_CU_CYCLES", "SQ_INST_LEVEL_VMEM", "SQ_INST_CYCLES_VMEM_RD",
+                  "SQ_INST_CYCLES_VMEM_WR", "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_WR_TA_DATA_FIFO_FULL",
+                  "SQ_THREAD_CYCLES_VALU"):
             if c in m:
                 row[c] = m[c]
         if "TCC_HIT_sum" in m:
