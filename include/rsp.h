@@ -183,6 +183,18 @@ int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t
                  const rsp_cfar_params* cfar, uint8_t* d_flag, uint8_t* d_flagV,
                  void* stream);
 
+/* Sliding-window stream (MTD/main_produce_dataset_win_xzr_v2.m:94-144; replaces its
+ * beam x window loop of fun_MTD_produce calls at :117-136).  d_frames: [beams][frames+1][P][R]
+ * consecutive frames of each beam.  For frame pair (n, n+1) and window i < win, the CPI is rows
+ * [s_i, s_i + P) of [frame n; frame n+1] with s_i = round(i*P/win) (0-based, :123).  Outputs
+ * [beams][frames][win][P][R_out] (MTD_win_all_beams{b}(i+1,:,:) per frame, :131-139); with
+ * cfar != NULL each window also runs executeCFAR (flags in the same layout).  Pulse
+ * compression is row-wise, so each frame's PC is computed once and shared by its windows
+ * (exact).  win <= 16. */
+int rsp_window_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_frames, int32_t dtype, int64_t beams,
+                               int64_t frames, int32_t win, const rsp_cfar_params* cfar,
+                               float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV, void* stream);
+
 /* Pulse compression alone (fun_lss_pulse_compression), for tests and staged use:
  * d_pc = [batch][P][R_out] complex float32. */
 int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, void* d_pc,

@@ -679,19 +679,13 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
     return RSP_OK;
 }
 
-int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,
-                        const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                        void* stream) {
-    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: null ctx");
-    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "context was created for CFAR only (params == NULL)");
-    if (!d_echo || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: bad echo/batch");
-    if (dtype != RSP_C64 && dtype != RSP_C32F16)
-        return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: device dtype must be RSP_C64 or RSP_C32F16");
-    if (cfar && !d_flag) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: CFAR requested without d_flag");
-    if (!cfar && !d_rdm) return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_dev: no output requested");
-    if (batch == 0) return RSP_OK;
-    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
-    hipStream_t s = (hipStream_t)stream;
+// The chain over `units` on stream s.  win == 0: a unit is one CPI ([P][R] input rows).
+// win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
+// frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
+// frames plus the look-ahead frame once, and every window reads its rows from that PC.
+static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
+                     const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                     hipStream_t s) {
     const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out;
     const size_t esz = dtype == RSP_C64 ? 8 : 4;
     rsp::MtdArgs m = ctx->mtd;
@@ -702,18 +696,28 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
     } else {
         m.cv.enabled = 0;
     }
-    const int64_t chunk = chunk_of(ctx, batch);
-    const int64_t nchunks = (batch + chunk - 1) / chunk;
+    const int64_t ocpi = win > 0 ? win : 1;               // output CPIs per unit
+    m.nwin = win;
+    for (int i = 0; i < win; ++i) m.win_start[i] = (int)mround((double)i * P / win);
+    int64_t cu = chunk_of(ctx, units * ocpi);              // CPIs per chunk
+    if (win > 0) {
+        cu = cu / ocpi;
+        if (cu < 8) cu = 8;                                // look-ahead PC overhead <= 1/8
+    }
+    if (cu > units) cu = units;
+    const int64_t nchunks = (units + cu - 1) / cu;
     const int ns = (int)(ctx->nstreams < nchunks ? ctx->nstreams : nchunks);
-    const size_t cells = (size_t)chunk * P * Ro;   // per chunk slot
-    int rc = ensure(ctx, ctx->scratch_pc, (size_t)ns * cells * sizeof(float2));
+    const size_t plane = (size_t)P * Ro;
+    const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
+    const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * P;
+    int rc = ensure(ctx, ctx->scratch_pc, (size_t)ns * pcrows * Ro * sizeof(float2));
     if (rc) return rc;
+    int nreg = 0, reg = 0;
     if (cfar) {
         // fused range stage: per-lane hit lists, one region per MTD workgroup sized to its
         // cells (no overflow, no global atomics), and per-workgroup counts
         if (cells > 0xffffffffull) return fail(ctx, RSP_ERR_UNSUPPORTED, "chunk too large for 32-bit hit indices");
-        int nreg = 0, reg = 0;
-        rsp::mtd_regions((int)P, (int)Ro, (int)chunk, &nreg, &reg);
+        rsp::mtd_regions((int)P, (int)Ro, (int)(cu * ocpi), &nreg, &reg);
         rc = ensure(ctx, ctx->hit_list, (size_t)ns * nreg * reg * sizeof(uint32_t));
         if (rc) return rc;
         rc = ensure(ctx, ctx->hit_ctr, (size_t)ns * nreg * sizeof(uint32_t));
@@ -738,36 +742,82 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
         }
     }
     for (int64_t k = 0; k < nchunks; ++k) {
-        const int64_t c0 = k * chunk;
-        const int64_t n = batch - c0 < chunk ? batch - c0 : chunk;
+        const int64_t u0 = k * cu;
+        const int64_t n = units - u0 < cu ? units - u0 : cu;
+        const int64_t ncpi = n * ocpi;                     // CPIs this chunk produces
+        const size_t o0 = (size_t)u0 * ocpi * plane;      // output offset
         const int lane = (int)(k % ns);
         hipStream_t ls = lanes[lane];
-        const char* ein = (const char*)d_echo + (size_t)c0 * P * R * esz;
-        float* rdm = d_rdm ? d_rdm + (size_t)c0 * P * Ro : (float*)ctx->tmp_rdm.p + lane * cells;
-        uint8_t* fv = (cfar && d_flagV) ? d_flagV + (size_t)c0 * P * Ro : nullptr;
-        float2* pcs = (float2*)ctx->scratch_pc.p + lane * cells;
-        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * P, ls));
-        int nreg = 0, reg = 0;
+        const char* ein = (const char*)d_echo + (size_t)u0 * P * R * esz;
+        float* rdm = d_rdm ? d_rdm + o0 : (float*)ctx->tmp_rdm.p + lane * cells;
+        uint8_t* fv = (cfar && d_flagV) ? d_flagV + o0 : nullptr;
+        float2* pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
+        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * P, ls));
         if (cfar) {
-            rsp::mtd_regions((int)P, (int)Ro, (int)chunk, &nreg, &reg);
-            m.flag = d_flag + (size_t)c0 * P * Ro;
+            m.flag = d_flag + o0;
             m.rflag = cr.rflag;
             m.hits = (uint32_t*)ctx->hit_list.p + (size_t)lane * nreg * reg;
             m.hit_count = (uint32_t*)ctx->hit_ctr.p + (size_t)lane * nreg;
-            rsp::mtd_regions((int)P, (int)Ro, (int)n, &nreg, &reg);   // this chunk's workgroups
         }
         if (cfar && cr.rflag)   // background of the flag plane; the range stage writes the 1s
-            HIP_TRY(ctx, hipMemsetAsync(m.flag, 0, (size_t)n * P * Ro, ls));
-        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)n, m, ls); }));
+            HIP_TRY(ctx, hipMemsetAsync(m.flag, 0, (size_t)ncpi * plane, ls));
+        HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
+            int nr = 0, rg = 0;
+            rsp::mtd_regions((int)P, (int)Ro, (int)ncpi, &nr, &rg);   // this chunk's workgroups
             HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] {
-                return rsp::launch_cfar_hits(rdm, m.flag, m.hits, m.hit_count, nreg, reg, cr, ls);
+                return rsp::launch_cfar_hits(rdm, m.flag, m.hits, m.hit_count, nr, rg, cr, ls);
             }));
         }
     }
     for (int i = 1; i < ns; ++i) {
         HIP_TRY(ctx, hipEventRecord(ctx->ev_join[i - 1], lanes[i]));
         HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join[i - 1], 0));
+    }
+    return RSP_OK;
+}
+
+static int check_chain_args(rsp_ctx* ctx, const char* fn, const void* d_echo, int32_t dtype, int64_t n,
+                            const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "%s: null ctx", fn);
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "context was created for CFAR only (params == NULL)");
+    if (!d_echo || n < 0) return fail(ctx, RSP_ERR_ARG, "%s: bad input pointer/count", fn);
+    if (dtype != RSP_C64 && dtype != RSP_C32F16)
+        return fail(ctx, RSP_ERR_ARG, "%s: device dtype must be RSP_C64 or RSP_C32F16", fn);
+    if (cfar && !d_flag) return fail(ctx, RSP_ERR_ARG, "%s: CFAR requested without d_flag", fn);
+    if (!cfar && !d_rdm) return fail(ctx, RSP_ERR_ARG, "%s: no output requested", fn);
+    return RSP_OK;
+}
+
+int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,
+                        const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                        void* stream) {
+    int rc = check_chain_args(ctx, "rsp_pc_mtd_cfar_dev", d_echo, dtype, batch, cfar, d_rdm, d_flag);
+    if (rc) return rc;
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    return run_chain(ctx, d_echo, dtype, batch, 0, cfar, d_rdm, d_flag, d_flagV, (hipStream_t)stream);
+}
+
+int rsp_window_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_frames, int32_t dtype, int64_t beams, int64_t frames,
+                               int32_t win, const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag,
+                               uint8_t* d_flagV, void* stream) {
+    int rc = check_chain_args(ctx, "rsp_window_pc_mtd_cfar_dev", d_frames, dtype, frames, cfar, d_rdm, d_flag);
+    if (rc) return rc;
+    if (beams < 0) return fail(ctx, RSP_ERR_ARG, "rsp_window_pc_mtd_cfar_dev: beams %lld < 0", (long long)beams);
+    if (win < 1 || win > rsp::RSP_MAX_WIN)
+        return fail(ctx, RSP_ERR_ARG, "rsp_window_pc_mtd_cfar_dev: win %d outside 1..%d", win, rsp::RSP_MAX_WIN);
+    if (frames == 0 || beams == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out;
+    const size_t esz = dtype == RSP_C64 ? 8 : 4;
+    const size_t in_beam = (size_t)(frames + 1) * P * R * esz;    // bytes of one beam's frames
+    const size_t out_beam = (size_t)frames * win * P * Ro;         // cells of one beam's windows
+    for (int64_t b = 0; b < beams; ++b) {
+        rc = run_chain(ctx, (const char*)d_frames + b * in_beam, dtype, frames, win, cfar,
+                       d_rdm ? d_rdm + b * out_beam : nullptr, d_flag ? d_flag + b * out_beam : nullptr,
+                       d_flagV ? d_flagV + b * out_beam : nullptr, (hipStream_t)stream);
+        if (rc) return rc;
     }
     return RSP_OK;
 }

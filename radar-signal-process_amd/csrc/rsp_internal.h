@@ -61,8 +61,15 @@ struct CfarVArgs {
     int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
 };
 
+constexpr int RSP_MAX_WIN = 16;
+
 struct MtdArgs {
     int P, R_out;
+    // Sliding-window mode (main_produce_dataset_win_xzr_v2.m:117-131): launch CPI j is window
+    // j % nwin of frame j / nwin; its P pulses are PC rows [n*P + win_start[j % nwin], +P) of
+    // a frame-contiguous PC buffer.  nwin == 0: CPI j reads rows [j*P, (j+1)*P).
+    int nwin;
+    int win_start[RSP_MAX_WIN];
     int shift;           // fftshift offset floor(P/2), or 0
     int z_lo, z_hi;      // fun_0v_pressing rows zeroed in the RDM
     const float* win;    // slow-time window, P entries

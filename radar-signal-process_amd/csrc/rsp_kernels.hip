@@ -765,7 +765,9 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     const bool rv = r < (int)R;
     const uint32_t plane = (uint32_t)P * R;
     const uint32_t cell = (uint32_t)g * R + (uint32_t)r;        // element (g, r) of a plane
-    const auto src = buf_rsrc(pc + cpi * plane, plane * 8u);
+    size_t row0 = cpi * (size_t)P;                               // first PC row of this CPI
+    if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)P + a.win_start[cpi % a.nwin];
+    const auto src = buf_rsrc(pc + row0 * R, plane * 8u);
     const uint32_t vo_in = rv ? cell * 8u : kOob;
     float2 u[E];
 #pragma unroll

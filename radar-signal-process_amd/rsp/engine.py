@@ -169,6 +169,39 @@ class Engine:
             self._stream_handle(stream))
         capi.check(rc, self.ctx)
 
+    def window_dev(self, frames, win, rdm=None, flag=None, flagV=None, cfar=None, stream=None):
+        """Sliding-window stream (main_produce_dataset_win_xzr_v2.m:94-144).
+        frames: [beams, F+1, P, R] complex64 (or [..., 2] float16 I/Q) consecutive frames;
+        outputs [beams, F, win, P, R_out] -- window i of frame pair (n, n+1) is rows
+        [round(i*P/win), +P) of [frame n; frame n+1]."""
+        import torch
+        if not frames.is_cuda or not frames.is_contiguous():
+            raise ValueError("frames must be a contiguous CUDA tensor")
+        if frames.dtype == torch.complex64:
+            dt, lead = capi.RSP_C64, tuple(frames.shape[:2])
+            tail = tuple(frames.shape[2:])
+        elif frames.dtype == torch.float16 and frames.shape[-1] == 2:
+            dt, lead = capi.RSP_C32F16, tuple(frames.shape[:2])
+            tail = tuple(frames.shape[2:4])
+        else:
+            raise ValueError("frames must be complex64 [beams, F+1, P, R] or float16 [beams, F+1, P, R, 2]")
+        if len(lead) != 2 or tail != (self.spec.P, self.spec.R) or lead[1] < 2:
+            raise ValueError("frames is %s, engine expects [beams, F+1>=2, %d, %d]"
+                             % (tuple(frames.shape), self.spec.P, self.spec.R))
+        beams, nf = lead[0], lead[1] - 1
+        want = (beams, nf, int(win), self.spec.P, self.spec.R_out)
+        for t, dtp in ((rdm, torch.float32), (flag, torch.uint8), (flagV, torch.uint8)):
+            if t is not None and (tuple(t.shape) != want or t.dtype != dtp or not t.is_contiguous() or not t.is_cuda):
+                raise ValueError("output tensor must be contiguous CUDA %s of shape %s" % (dtp, want))
+        cp = cfar.to_c() if cfar is not None else None
+        rc = self.lib.rsp_window_pc_mtd_cfar_dev(
+            self.ctx, C.c_void_p(frames.data_ptr()), dt, beams, nf, int(win), C.byref(cp) if cp is not None else None,
+            C.c_void_p(rdm.data_ptr()) if rdm is not None else None,
+            C.c_void_p(flag.data_ptr()) if flag is not None else None,
+            C.c_void_p(flagV.data_ptr()) if flagV is not None else None,
+            self._stream_handle(stream))
+        capi.check(rc, self.ctx)
+
     def pc_dev(self, echo, out, stream=None):
         """Pulse compression alone: out [batch, P, R_out] complex64."""
         import torch

@@ -1,0 +1,160 @@
+"""GPU tests of the sliding-window stream and of the fused
+range-CFAR variants of the chain (flagV not requested; rFlag = 0).
+
+Window i of frame pair (n, n+1) is rows [round(i*P/win), +P) of [frame n; frame n+1]
+(MTD/main_produce_dataset_win_xzr_v2.m:117-131).  Pulse compression is row-wise, so the
+engine computes each frame's PC once and every window reads it: the windowed outputs must be
+BIT-identical to the plain chain run on the sliced echo, and within the RDM / CFAR bars of
+SURVEY.md §8d against the fp64 oracle.
+"""
+import numpy as np
+import pytest
+
+from _util import NEAR_TOL, RDM_TOL, flag_mismatch, oracle_flags, oracle_rdm, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _mround(x):
+    return int(np.floor(x + 0.5))
+
+
+def _windows(frames, win):
+    """[beams, F+1, P, R] -> [beams, F, win, P, R] by the reference's slicing."""
+    beams, nf1, P, R = frames.shape
+    out = np.empty((beams, nf1 - 1, win, P, R), dtype=frames.dtype)
+    for b in range(beams):
+        for n in range(nf1 - 1):
+            pair = np.concatenate([frames[b, n], frames[b, n + 1]], axis=0)
+            for i in range(win):
+                s = _mround(i * P / win)
+                out[b, n, i] = pair[s:s + P]
+    return out
+
+
+@pytest.mark.parametrize("P,R,beams,nf,win,chunk", [(64, 1024, 2, 3, 4, 0), (128, 4096, 1, 2, 4, 0),
+                                                     (64, 1024, 1, 5, 3, 8), (96, 1024, 1, 2, 5, 0)])
+def test_window_bit_exact_vs_sliced_chain(torch_cuda, P, R, beams, nf, win, chunk):
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    spec = presets.v2(P, R)
+    eng = Engine(spec, device=0, chunk=chunk)
+    cf = presets.default_cfar(spec)
+    frames = synth.echo_numpy(spec, beams * (nf + 1), seed=1004).reshape(beams, nf + 1, P, R)
+    d_frames = torch.from_numpy(frames).cuda()
+    shp = (beams, nf, win, P, spec.R_out)
+    d_rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.window_dev(d_frames, win, rdm=d_rdm, flag=d_flag, cfar=cf)
+    sliced = _windows(frames, win).reshape(-1, P, R)
+    d_sl = torch.from_numpy(np.ascontiguousarray(sliced)).cuda()
+    n = sliced.shape[0]
+    e_rdm = torch.empty((n, P, spec.R_out), dtype=torch.float32, device="cuda")
+    e_flag = torch.empty((n, P, spec.R_out), dtype=torch.uint8, device="cuda")
+    eng.run_dev(d_sl, rdm=e_rdm, flag=e_flag, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(d_rdm.reshape(n, P, -1), e_rdm)
+    assert torch.equal(d_flag.reshape(n, P, -1), e_flag)
+    eng.close()
+
+
+def test_window_parity_vs_oracle(torch_cuda):
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    P, R, win = 64, 1024, 4
+    spec = presets.v2(P, R)
+    eng = Engine(spec, device=0)
+    cf = presets.default_cfar(spec)
+    frames = synth.echo_numpy(spec, 3, seed=1044).reshape(1, 3, P, R)
+    d_frames = torch.from_numpy(frames).cuda()
+    shp = (1, 2, win, P, R)
+    d_rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.window_dev(d_frames, win, rdm=d_rdm, flag=d_flag, cfar=cf)
+    torch.cuda.synchronize()
+    sliced = _windows(frames, win).reshape(-1, P, R)
+    rdm = oracle_rdm("v2", sliced)
+    got = d_rdm.cpu().numpy().reshape(-1, P, R)
+    assert rel_err(got, rdm) < RDM_TOL
+    flag, _, amb = oracle_flags(rdm, cf)
+    hard, soft = flag_mismatch(d_flag.cpu().numpy().reshape(-1, P, R), flag, amb)
+    assert hard == 0 and soft <= 2, (hard, soft)
+    assert flag.sum() > 0
+    # window 0 of pair n is frame n itself
+    assert rel_err(got[0], oracle_rdm("v2", frames[0, :1])[0]) < RDM_TOL
+    eng.close()
+
+
+def test_window_errors(torch_cuda):
+    torch = torch_cuda
+    from rsp import presets
+    from rsp._capi import RspError
+    from rsp.engine import Engine
+    eng = Engine(presets.v2(64, 1024), device=0)
+    d = torch.zeros((1, 2, 64, 1024), dtype=torch.complex64, device="cuda")
+    r = torch.empty((1, 1, 17, 64, 1024), dtype=torch.float32, device="cuda")
+    with pytest.raises(RspError):
+        eng.window_dev(d, 17, rdm=r)         # win > 16
+    with pytest.raises(ValueError):
+        eng.window_dev(d[:, :1].contiguous(), 4, rdm=r)   # needs >= 2 frames
+    eng.close()
+
+
+def test_chain_without_flagV_matches(torch_cuda):
+    """The hot path (flagV not requested: no Doppler-flag plane is written) gives the same
+    flags as the path that also returns flagV."""
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    for P, R in ((64, 1024), (128, 4096)):
+        spec = presets.v2(P, R)
+        eng = Engine(spec, device=0)
+        cf = presets.default_cfar(spec)
+        echo = torch.from_numpy(synth.echo_numpy(spec, 3, seed=1005)).cuda()
+        shp = (3, P, R)
+        f1 = torch.empty(shp, dtype=torch.uint8, device="cuda")
+        f2 = torch.empty(shp, dtype=torch.uint8, device="cuda")
+        fv = torch.empty(shp, dtype=torch.uint8, device="cuda")
+        r1 = torch.empty(shp, dtype=torch.float32, device="cuda")
+        eng.run_dev(echo, rdm=r1, flag=f1, cfar=cf)
+        eng.run_dev(echo, flag=f2, flagV=fv, cfar=cf)     # internal RDM buffer
+        torch.cuda.synchronize()
+        assert torch.equal(f1, f2)
+        assert int(f1.sum()) > 0 and int(fv.sum()) > int(f1.sum())
+        eng.close()
+
+
+def test_chain_rflag0_is_flagV(torch_cuda):
+    """rCFARDetect_Flag = 0: executeCFAR returns flag = flagV (executeCFAR.m:91)."""
+    torch = torch_cuda
+    import dataclasses
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    P, R = 64, 1024
+    spec = presets.v2(P, R)
+    eng = Engine(spec, device=0)
+    cf = dataclasses.replace(presets.default_cfar(spec), rFlag=0)
+    echo_np = synth.echo_numpy(spec, 2, seed=1006)
+    echo = torch.from_numpy(echo_np).cuda()
+    shp = (2, P, R)
+    f = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    fv = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    eng.run_dev(echo, rdm=rdm, flag=f, flagV=fv, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(f, fv)
+    ordm = oracle_rdm("v2", echo_np)
+    flag, flagV, amb = oracle_flags(ordm, cf)
+    assert np.array_equal(flag, flagV)
+    hard, soft = flag_mismatch(f.cpu().numpy(), flag, amb)
+    assert hard == 0 and soft <= 2
+    eng.close()
