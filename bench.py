@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: CPIs/s through PC -> MTD -> 0-v -> 2-D CA-CFAR (BASELINE.json metric).
 
-Workload (config c3 of BASELINE.json): 128 pulses x 4096 range bins, complex fp32 echo,
-batch 1024 CPIs per GPU, `v2` preset (fun_MTD_produce's 3-segment pulse compression,
-kaiser-8 MTD with fftshift, 0-v /150) followed by main_cfar's /20 0-v and executeCFAR per
-PC segment (ref 5, guard 7, T 5, GO, range CFAR on).  A step is one pass of the chain
-over the batch, inputs resident in HBM.  Synthetic echoes (SURVEY.md §8d recipe, noise
-drawn on the GPU).
+Default workload (config c3 of BASELINE.json, the metric's config): 128 pulses x 4096 range
+bins, complex fp32 echo, batch 1024 CPIs per GPU, `v2` preset (fun_MTD_produce's 3-segment
+pulse compression, kaiser-8 MTD with fftshift, 0-v /150) followed by main_cfar's /20 0-v and
+executeCFAR per PC segment (ref 5, guard 7, T 5, GO, range CFAR on).  A step is one pass of
+the chain over the batch, inputs resident in HBM.  Synthetic echoes (SURVEY.md §8d recipe,
+noise drawn on the GPU).  --config c2 / c4 / c5 select the other BASELINE configs (c4: the
+sliding-window stream, unit = window; c5: 512 x 16384 fp16 I/Q).
 
 Multi-GPU: one process per GPU (torchrun); each rank owns a contiguous shard of the CPI
 stream (weak scaling, no data-path collective: CPIs are independent); the only collectives
@@ -27,26 +28,45 @@ METRIC = "CPIs/sec (4096 range × 128 pulse) through PC→MTD→CFAR; achieved H
 HBM_PEAK_GBPS = 8000.0
 
 
+# BASELINE.json configs.  mode "window": batch = frame pairs per GPU per step,
+# each giving `win` windowed CPIs (MTD/main_produce_dataset_win_xzr_v2.m:94-144).
+CONFIGS = {
+    "c2": dict(P=128, R=4096, batch=256, cfar=False, half=False, win=0),
+    "c3": dict(P=128, R=4096, batch=1024, cfar=True, half=False, win=0),
+    "c4": dict(P=256, R=8192, batch=32, cfar=True, half=False, win=4),
+    "c5": dict(P=512, R=16384, batch=64, cfar=True, half=True, win=0),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3, help=">= 1 (the first warmup step counts launches)")
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--preset", default="v2", choices=["v2", "dmx"])
-    ap.add_argument("--P", type=int, default=128)
-    ap.add_argument("--R", type=int, default=4096)
-    ap.add_argument("--batch", type=int, default=1024, help="CPIs per GPU per step")
-    ap.add_argument("--no-cfar", action="store_true", help="PC + MTD only (config c2)")
-    ap.add_argument("--half", action="store_true", help="fp16 I/Q input (config c5 style)")
+    ap.add_argument("--P", type=int, default=None)
+    ap.add_argument("--R", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None, help="CPIs (window mode: frame pairs) per GPU per step")
+    ap.add_argument("--no-cfar", action="store_true", help="PC + MTD only")
+    ap.add_argument("--half", action="store_true", help="fp16 I/Q input")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--profile-every", type=int, default=8, help="bracket every N-th kernel launch with events")
-    return ap.parse_args()
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    args.P = args.P or cfg["P"]
+    args.R = args.R or cfg["R"]
+    args.batch = args.batch or cfg["batch"]
+    args.no_cfar = args.no_cfar or not cfg["cfar"]
+    args.half = args.half or cfg["half"]
+    args.win = cfg["win"]
+    return args
 
 
-def cpu_baseline(spec, cfar, seconds):
+def cpu_baseline(spec, cfar, seconds, unit="CPI/s"):
     """fp64 C restatement (oracle/rsp_oracle.c, OpenMP over CPIs) on a bounded sample."""
     if seconds <= 0:
         return None
@@ -71,7 +91,7 @@ def cpu_baseline(spec, cfar, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": done / el, "unit": "CPI/s", "cores": threads, "kind": "port",
+    return {"value": done / el, "unit": unit, "cores": threads, "kind": "port",
             "sample": "%d CPIs (%d x %d, %s preset%s) in %.1f s: a pool of %d distinct synthetic CPIs "
                       "cycled; fp64 C restatement of the MATLAB chain (MATLAB itself is not available)"
                       % (done, spec.P, spec.R, spec.name, " + CFAR" if c else "", el, pool_n)}
@@ -106,16 +126,29 @@ def main():
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
-    B, P, R = args.batch, spec.P, spec.R_out
-    # contiguous shard of the CPI stream per rank: seed = 1000 + config id 3 + first CPI index
-    lo, _ = shard.weak_shard(B, rank)
-    echo = synth.echo_torch(spec, B, seed=1003 + lo, device=dev, half=args.half)
-    rdm = torch.empty((B, P, R), dtype=torch.float32, device=dev)
-    flag = torch.empty((B, P, R), dtype=torch.uint8, device=dev) if cfar else None
+    B, P, R, win = args.batch, spec.P, spec.R_out, args.win
+    units = B * win if win else B                   # CPIs (windows) per GPU per step
+    # contiguous shard of the stream per rank (weak scaling): seed = 1000 + config id + first
+    # unit index; window mode also holds the look-ahead frame of its last pair (halo)
+    cfg_id = int(args.config[1:])
+    lo, hi = shard.weak_shard(B, rank)
+    if win:
+        flo, fhi = shard.window_frames(lo, hi)
+        echo = synth.echo_torch(spec, fhi - flo, seed=1000 + cfg_id + flo, device=dev, half=args.half)
+        echo = echo.reshape((1, fhi - flo) + tuple(echo.shape[1:]))
+        oshape = (1, B, win, P, R)
+    else:
+        echo = synth.echo_torch(spec, B, seed=1000 + cfg_id + lo, device=dev, half=args.half)
+        oshape = (B, P, R)
+    rdm = torch.empty(oshape, dtype=torch.float32, device=dev)
+    flag = torch.empty(oshape, dtype=torch.uint8, device=dev) if cfar else None
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        eng.run_dev(echo, rdm=rdm, flag=flag, cfar=cfar, stream=stream)
+        if win:
+            eng.window_dev(echo, win, rdm=rdm, flag=flag, cfar=cfar, stream=stream)
+        else:
+            eng.run_dev(echo, rdm=rdm, flag=flag, cfar=cfar, stream=stream)
 
     def barrier():
         if world > 1:
@@ -157,21 +190,23 @@ def main():
 
     if rank == 0:
         esz = 4 if args.half else 8
-        in_b, rdm_b, flag_b = P * spec.R * esz, P * R * 4, (P * R if cfar else 0)
-        cpi_bytes = in_b + rdm_b + flag_b              # SURVEY.md §8d algorithmic bytes per CPI
-        total_cpis = world * B * args.steps
-        value = total_cpis / elapsed
-        per_gpu_cpis_s = B * args.steps / (gpu_ms / 1e3)
-        chain_gbps = per_gpu_cpis_s * cpi_bytes / 1e9
-        tag = "%s_P%d_R%d%s%s" % (args.preset, args.P, args.R, "" if cfar else "_nocfar", "_f16" if args.half else "")
+        in_b = P * spec.R * esz / (win if win else 1)   # window mode: each frame feeds `win` windows
+        rdm_b, flag_b = P * R * 4, (P * R if cfar else 0)
+        cpi_bytes = int(in_b + rdm_b + flag_b)          # SURVEY.md §8d algorithmic bytes per CPI / window
+        total_units = world * units * args.steps
+        value = total_units / elapsed
+        per_gpu_units_s = units * args.steps / (gpu_ms / 1e3)
+        chain_gbps = per_gpu_units_s * cpi_bytes / 1e9
+        tag = "%s_P%d_R%d%s%s%s" % (args.preset, args.P, args.R, "" if cfar else "_nocfar",
+                                    "_f16" if args.half else "", "_win%d" % win if win else "")
         pmc = pmc_traffic(tag)
         # Dominant kernel (largest device time per step): achieved = §8d bytes per CPI x CPIs per
         # launch / its mean launch duration (HIP events on its launch stream); traffic = HBM-side
         # bytes per launch from the committed PMC summary.
         roof = {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": None, "traffic": None, "alg_bytes_per_cpi": cpi_bytes,
+                "frac": None, "traffic": None, "alg_bytes_per_unit": cpi_bytes,
                 "chain": {"achieved": round(chain_gbps, 1), "frac": round(chain_gbps / HBM_PEAK_GBPS, 4),
-                          "note": "whole step: CPIs/s x alg bytes per CPI"}}
+                          "note": "whole step: units/s x alg bytes per unit"}}
         if kernels:
             ks = {}
             for name, (ms, n) in kernels.items():
@@ -179,11 +214,13 @@ def main():
                 ks[name] = {"avg_us": round(avg_us, 2), "sampled_launches": n,
                             "launches_per_step": launches_per_step.get(name)}
             dom = max(kernels, key=lambda k: kernels[k][0])
-            cpl = B / launches_per_step[dom]           # CPIs per launch (chunk)
+            cpl = units / launches_per_step[dom]       # CPIs (windows) per launch
+            if dom == "pc_kernel" and win:
+                cpl = B / launches_per_step[dom] * win   # one PC launch serves its frames' windows
             avg_s = kernels[dom][0] / 1e3 / kernels[dom][1]
             ach = cpi_bytes * cpl / avg_s / 1e9
             roof.update({"kernel": dom, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "cpis_per_launch": cpl, "alg_bytes_per_launch": int(cpi_bytes * cpl),
+                         "units_per_launch": cpl, "alg_bytes_per_launch": int(cpi_bytes * cpl),
                          "avg_launch_us": round(avg_s * 1e6, 2)})
             if pmc and dom in pmc.get("kernels", {}):
                 kp = pmc["kernels"][dom]
@@ -199,11 +236,25 @@ def main():
         achieved = chain_gbps
         cpu = None
         if world == 1:
-            cpu = cpu_baseline(spec, cfar, args.cpu_seconds)
+            # window mode: the reference runs fun_MTD_produce per window, so its rate is CPIs/s
+            cpu = cpu_baseline(spec, cfar, args.cpu_seconds, unit="window/s" if win else "CPI/s")
+        mode = "%s: %d pulses x %d range bins, %s, preset %s, PC->MTD->0v%s" % (
+            args.config, P, spec.R,
+            ("%d frame pairs x %d windows per GPU per step (sliding window, PC shared by windows)" % (B, win))
+            if win else "%d CPIs per GPU per step" % B, args.preset,
+            "->2D CA-CFAR (executeCFAR per PC segment)" if cfar else "")
+        if args.config == "c3" and not win and P == 128 and spec.R == 4096 and cfar:
+            metric, unit = METRIC, "CPI/s"
+        elif win:
+            metric, unit = "windows/sec (%d range x %d pulse, %d windows per frame pair) through PC->MTD%s" % (
+                spec.R, P, win, "->CFAR" if cfar else ""), "window/s"
+        else:
+            metric, unit = "CPIs/sec (%d range x %d pulse) through PC->MTD%s" % (
+                spec.R, P, "->CFAR" if cfar else ""), "CPI/s"
         out = {
-            "metric": METRIC,
+            "metric": metric,
             "value": round(value, 1),
-            "unit": "CPI/s",
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -213,10 +264,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if not args.half else "f32 (fp16 I/Q storage)",
             "data": "synthetic (SURVEY.md §8d echo: 3 targets + zero-Doppler clutter + CN(0,1) noise, GPU-drawn)",
-            "config": {"workload": "c3: %d pulses x %d range bins, %d CPIs per GPU per step, preset %s, "
-                                   "PC->MTD->0v%s" % (P, spec.R, B, args.preset,
-                                                      "->2D CA-CFAR (executeCFAR per PC segment)" if cfar else ""),
-                       "pulses": P, "range_bins": spec.R, "batch_per_gpu": B, "preset": args.preset,
+            "config": {"workload": mode, "pulses": P, "range_bins": spec.R, "batch_per_gpu": B,
+                       "windows_per_pair": win or None, "preset": args.preset,
                        "input": "c32f16" if args.half else "c64",
                        "parallelism": "frame-sharded x%d, no collective" % world},
             "hbm_GBps_per_gpu": round(achieved, 1),
