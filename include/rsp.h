@@ -114,6 +114,17 @@ typedef struct {
     int32_t zero_v_div;    /* fun_0v_pressing divisor (150 in MTD/fun_0v_pressing.m:22);
                               0 = no suppression */
     rsp_pc_segment seg[RSP_MAX_SEG];
+    /* ---- DMX slow-time variant (DMX_SignalProcessing_main_xzr.m:208-229,414-426,462-465);
+     *      all zero = the fun_Process_MTD path above ---- */
+    int64_t mtd_nfft;      /* Doppler FFT length V (fft(pc.*w, V, 1)); 0 = P.  V > P zero-pads
+                              the pulses (DMX mtd_FFT_num = 2048 over prtNum = 1536).  The RDM
+                              and the CFAR work on V rows. */
+    int32_t beams;         /* 0/1: one beam.  2: the DMX left/right pair -- echo [2][P][R] per
+                              CPI (beam 0 = left), RDM = |X_L| + |X_R| (:421-422), optional
+                              difference |X_R| - |X_L| (:425-426, rsp_pc_mtd_cfar_diff_dev) */
+    int32_t zero_ends;     /* 0: off.  n > 0: zero RDM rows [0, n) and [V-n+1, V) -- the DMX
+                              zeroSetFlagMTD with n = MTD_0_num + 1 (:463-465); replaces
+                              fun_0v_pressing (zero_v_div) for the RDM */
 } rsp_params;
 
 typedef struct {
@@ -182,6 +193,14 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
 int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t batch,
                  const rsp_cfar_params* cfar, uint8_t* d_flag, uint8_t* d_flagV,
                  void* stream);
+
+/* rsp_pc_mtd_cfar_dev for a two-beam context (rsp_params.beams == 2): d_echo
+ * [batch][2][P][R]; d_sum [batch][V][R_out] = |X_L| + |X_R| (the RDM, zeroSetFlagMTD
+ * applied); d_diff (nullable) = |X_R| - |X_L|; CFAR runs on the sum
+ * (DMX_SignalProcessing_main_xzr.m:414-472). */
+int rsp_pc_mtd_cfar_diff_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,
+                             const rsp_cfar_params* cfar, float* d_sum, float* d_diff,
+                             uint8_t* d_flag, uint8_t* d_flagV, void* stream);
 
 /* Sliding-window stream (MTD/main_produce_dataset_win_xzr_v2.m:94-144; replaces its
  * beam x window loop of fun_MTD_produce calls at :117-136).  d_frames: [beams][frames+1][P][R]

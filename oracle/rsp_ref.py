@@ -202,6 +202,22 @@ def dmx_pulse_compression(echo, p_short, nfft, H, fir_short=True):
 
 
 # ----------------------------------------------------------------------------- MTD
+def dmx_mtd_pair(pc_left, pc_right, nfft, m0):
+    """DMX_SignalProcessing_main_xzr.m:414-426,462-465 (MTD_win_TYPE 1): per beam
+    fft(pc .* hamming(prtNum), mtd_FFT_num, 1) -- no fftshift; sum = |L| + |R|,
+    diff = |R| - |L|; rows [1:M0+1, mtd_FFT_num-M0+1:mtd_FFT_num] (1-based) of the sum zeroed."""
+    pl = np.asarray(pc_left, np.complex128)
+    pr = np.asarray(pc_right, np.complex128)
+    w = hamming(pl.shape[0])[:, None]                                    # mtdWh (:211,227-228)
+    ml = np.abs(np.fft.fft(pl * w, nfft, axis=0))                        # :416,418
+    mr = np.abs(np.fft.fft(pr * w, nfft, axis=0))                        # :417,419
+    s = ml + mr                                                          # :421-422
+    d = mr - ml                                                          # :425-426
+    zero = list(range(0, m0 + 1)) + list(range(nfft - m0, nfft))         # zeroSetFlagMTD (:463)
+    s[zero, :] = 0.0                                                     # :464-465
+    return s, d
+
+
 def fun_Process_MTD(pc, window=None, nfft=None, shift=True):
     """MTD/fun_Process_MTD.m:13-40: for each range column,
     abs(fftshift(fft(col .* kaiser(P,8), P))).  The loop of :27-37 is kept."""

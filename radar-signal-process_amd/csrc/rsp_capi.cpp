@@ -37,6 +37,8 @@ struct rsp_ctx {
     bool pc_v2 = false;                 // per-segment specialised kernels (pc_mf_kernel)
     std::vector<rsp::PcMfArgs> pc_mf;   // one launch per matched-filter segment
     rsp::MtdArgs mtd{};
+    int64_t V = 0;                      // Doppler rows (rsp_params.mtd_nfft or P)
+    int beams = 1;                      // 2: DMX left/right pair
     size_t pc_lds = 0;
     int64_t chunk = 0;  // 0 = default
     int nstreams = 2;   // chunk pipelines (the caller's stream + nstreams-1 internal ones)
@@ -240,10 +242,17 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     if (p.P < 2 || p.R < 1 || p.R_out < 1 || p.R > (1 << 24) || p.R_out > (1 << 24))
         return fail(nullptr, RSP_ERR_SHAPE, "rsp_create: bad P=%lld R=%lld R_out=%lld",
                     (long long)p.P, (long long)p.R, (long long)p.R_out);
-    if (!rsp::mtd_size_supported((int)p.P))
+    const int64_t V = p.mtd_nfft ? p.mtd_nfft : p.P;
+    const int beams = p.beams ? p.beams : 1;
+    if (beams < 1 || beams > 2) return fail(nullptr, RSP_ERR_ARG, "rsp_create: beams=%d (1 or 2)", p.beams);
+    if (V < p.P)
+        return fail(nullptr, RSP_ERR_SHAPE, "rsp_create: mtd_nfft=%lld < P=%lld", (long long)V, (long long)p.P);
+    if (!rsp::mtd_size_supported((int)V, beams))
         return fail(nullptr, RSP_ERR_UNSUPPORTED,
-                    "rsp_create: P=%lld pulses not built (supported: 2^k or 3*2^k, 16..1536)",
-                    (long long)p.P);
+                    "rsp_create: Doppler length %lld (beams %d) not built (2^k or 3*2^k, 16..2048; two beams: "
+                    "512, 1024, 2048)", (long long)V, beams);
+    if (p.zero_ends < 0 || 2 * (int64_t)p.zero_ends > V)
+        return fail(nullptr, RSP_ERR_ARG, "rsp_create: zero_ends=%d out of range", p.zero_ends);
     if (p.nseg < 0 || p.nseg > RSP_MAX_SEG)
         return fail(nullptr, RSP_ERR_ARG, "rsp_create: nseg=%d out of range", p.nseg);
     if (p.window < RSP_WIN_KAISER || p.window > RSP_WIN_RECT)
@@ -405,17 +414,27 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
 
     // ---- MTD
     rsp::MtdArgs& m = ctx->mtd;
-    m.P = (int)p.P;
+    ctx->V = V;
+    ctx->beams = beams;
+    m.P = (int)V;            // Doppler FFT length; pulses beyond pin are the zero padding
+    m.pin = (int)p.P;
+    m.beams = beams;
     m.R_out = (int)p.R_out;
-    m.shift = p.fftshift ? (int)(p.P / 2) : 0;
-    zero_v_band(p.P, p.zero_v_div, &m.z_lo, &m.z_hi);
-    std::vector<double> w = make_window(p.window, p.window_beta, p.P);
-    std::vector<float> wf(w.begin(), w.end());
+    m.shift = p.fftshift ? (int)(V / 2) : 0;
+    if (p.zero_ends > 0) {   // rows [V-n+1, V) and [0, n): a band wrapping through row 0
+        m.z_lo = (int)(V - p.zero_ends + 1);
+        m.z_hi = (int)(V + p.zero_ends);
+    } else {
+        zero_v_band(V, p.zero_v_div, &m.z_lo, &m.z_hi);
+    }
+    std::vector<double> w = make_window(p.window, p.window_beta, p.P);   // window(P), zero-padded
+    std::vector<float> wf((size_t)V, 0.f);
+    for (int64_t i = 0; i < p.P; ++i) wf[(size_t)i] = (float)w[(size_t)i];
     float* dw = nullptr;
     int rc = upload(ctx, wf, &dw);
     if (rc) return bail(rc);
     m.win = dw;
-    rc = twiddles(ctx, (int)p.P, &m.tw);
+    rc = twiddles(ctx, (int)V, &m.tw);
     if (rc) return bail(rc);
     *out = ctx;
     return RSP_OK;
@@ -512,7 +531,7 @@ int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis) {
 static int64_t chunk_of(const rsp_ctx* ctx, int64_t batch) {
     int64_t c = ctx->chunk;
     if (c <= 0) {
-        const int64_t per = ctx->p.P * ctx->p.R_out * 8;
+        const int64_t per = (ctx->V > ctx->beams * ctx->p.P ? ctx->V : ctx->beams * ctx->p.P) * ctx->p.R_out * 8;
         c = (64ll << 20) / (per > 0 ? per : 1);
         if (c < 1) c = 1;
     }
@@ -685,13 +704,13 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
 // frames plus the look-ahead frame once, and every window reads its rows from that PC.
 static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
                      const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                     hipStream_t s) {
-    const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out;
+                     float* d_diff, hipStream_t s) {
+    const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out, V = ctx->V, NB = ctx->beams;
     const size_t esz = dtype == RSP_C64 ? 8 : 4;
     rsp::MtdArgs m = ctx->mtd;
     rsp::CfarRArgs cr{};
     if (cfar) {
-        int rc = build_cfar(ctx, cfar, P, Ro, &m.cv, &cr);
+        int rc = build_cfar(ctx, cfar, V, Ro, &m.cv, &cr);
         if (rc) return rc;
     } else {
         m.cv.enabled = 0;
@@ -707,9 +726,9 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
     if (cu > units) cu = units;
     const int64_t nchunks = (units + cu - 1) / cu;
     const int ns = (int)(ctx->nstreams < nchunks ? ctx->nstreams : nchunks);
-    const size_t plane = (size_t)P * Ro;
+    const size_t plane = (size_t)V * Ro;                  // output cells per CPI
     const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
-    const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * P;
+    const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * NB * P;
     int rc = ensure(ctx, ctx->scratch_pc, (size_t)ns * pcrows * Ro * sizeof(float2));
     if (rc) return rc;
     int nreg = 0, reg = 0;
@@ -717,7 +736,7 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
         // fused range stage: per-lane hit lists, one region per MTD workgroup sized to its
         // cells (no overflow, no global atomics), and per-workgroup counts
         if (cells > 0xffffffffull) return fail(ctx, RSP_ERR_UNSUPPORTED, "chunk too large for 32-bit hit indices");
-        rsp::mtd_regions((int)P, (int)Ro, (int)(cu * ocpi), &nreg, &reg);
+        rsp::mtd_regions((int)V, (int)Ro, (int)(cu * ocpi), &nreg, &reg);
         rc = ensure(ctx, ctx->hit_list, (size_t)ns * nreg * reg * sizeof(uint32_t));
         if (rc) return rc;
         rc = ensure(ctx, ctx->hit_ctr, (size_t)ns * nreg * sizeof(uint32_t));
@@ -748,11 +767,12 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
         const size_t o0 = (size_t)u0 * ocpi * plane;      // output offset
         const int lane = (int)(k % ns);
         hipStream_t ls = lanes[lane];
-        const char* ein = (const char*)d_echo + (size_t)u0 * P * R * esz;
+        const char* ein = (const char*)d_echo + (size_t)u0 * NB * P * R * esz;
         float* rdm = d_rdm ? d_rdm + o0 : (float*)ctx->tmp_rdm.p + lane * cells;
         uint8_t* fv = (cfar && d_flagV) ? d_flagV + o0 : nullptr;
         float2* pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
-        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * P, ls));
+        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls));
+        m.diff = d_diff ? d_diff + o0 : nullptr;
         if (cfar) {
             m.flag = d_flag + o0;
             m.rflag = cr.rflag;
@@ -764,7 +784,7 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
             int nr = 0, rg = 0;
-            rsp::mtd_regions((int)P, (int)Ro, (int)ncpi, &nr, &rg);   // this chunk's workgroups
+            rsp::mtd_regions((int)V, (int)Ro, (int)ncpi, &nr, &rg);   // this chunk's workgroups
             HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] {
                 return rsp::launch_cfar_hits(rdm, m.flag, m.hits, m.hit_count, nr, rg, cr, ls);
             }));
@@ -796,7 +816,19 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
     if (rc) return rc;
     if (batch == 0) return RSP_OK;
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
-    return run_chain(ctx, d_echo, dtype, batch, 0, cfar, d_rdm, d_flag, d_flagV, (hipStream_t)stream);
+    return run_chain(ctx, d_echo, dtype, batch, 0, cfar, d_rdm, d_flag, d_flagV, nullptr, (hipStream_t)stream);
+}
+
+int rsp_pc_mtd_cfar_diff_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,
+                             const rsp_cfar_params* cfar, float* d_sum, float* d_diff, uint8_t* d_flag,
+                             uint8_t* d_flagV, void* stream) {
+    int rc = check_chain_args(ctx, "rsp_pc_mtd_cfar_diff_dev", d_echo, dtype, batch, cfar, d_sum, d_flag);
+    if (rc) return rc;
+    if (ctx->beams != 2)
+        return fail(ctx, RSP_ERR_ARG, "rsp_pc_mtd_cfar_diff_dev: the context was created with beams=%d", ctx->beams);
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    return run_chain(ctx, d_echo, dtype, batch, 0, cfar, d_sum, d_flag, d_flagV, d_diff, (hipStream_t)stream);
 }
 
 int rsp_window_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_frames, int32_t dtype, int64_t beams, int64_t frames,
@@ -805,6 +837,8 @@ int rsp_window_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_frames, int32_t dtype
     int rc = check_chain_args(ctx, "rsp_window_pc_mtd_cfar_dev", d_frames, dtype, frames, cfar, d_rdm, d_flag);
     if (rc) return rc;
     if (beams < 0) return fail(ctx, RSP_ERR_ARG, "rsp_window_pc_mtd_cfar_dev: beams %lld < 0", (long long)beams);
+    if (ctx->beams != 1 || ctx->V != ctx->p.P)
+        return fail(ctx, RSP_ERR_ARG, "rsp_window_pc_mtd_cfar_dev: needs a one-beam context with mtd_nfft = P");
     if (win < 1 || win > rsp::RSP_MAX_WIN)
         return fail(ctx, RSP_ERR_ARG, "rsp_window_pc_mtd_cfar_dev: win %d outside 1..%d", win, rsp::RSP_MAX_WIN);
     if (frames == 0 || beams == 0) return RSP_OK;
@@ -816,7 +850,7 @@ int rsp_window_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_frames, int32_t dtype
     for (int64_t b = 0; b < beams; ++b) {
         rc = run_chain(ctx, (const char*)d_frames + b * in_beam, dtype, frames, win, cfar,
                        d_rdm ? d_rdm + b * out_beam : nullptr, d_flag ? d_flag + b * out_beam : nullptr,
-                       d_flagV ? d_flagV + b * out_beam : nullptr, (hipStream_t)stream);
+                       d_flagV ? d_flagV + b * out_beam : nullptr, nullptr, (hipStream_t)stream);
         if (rc) return rc;
     }
     return RSP_OK;
@@ -929,10 +963,10 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
     if (batch == 0) return RSP_OK;
     const void* d_echo = nullptr;
     int32_t d_dtype = RSP_C64;
-    rc = stage_echo(ctx, echo, dtype, layout, batch, &d_echo, &d_dtype);
+    rc = stage_echo(ctx, echo, dtype, layout, batch * ctx->beams, &d_echo, &d_dtype);   // [batch][beams][P][R]
     if (rc) return rc;
-    const int64_t Ro = ctx->p.R_out;
-    const size_t cells = (size_t)batch * P * Ro;
+    const int64_t Ro = ctx->p.R_out, V = ctx->V;
+    const size_t cells = (size_t)batch * V * Ro;
     if ((rc = ensure(ctx, ctx->st_rdm, cells * sizeof(float)))) return rc;
     if (cfar) {
         if ((rc = ensure(ctx, ctx->st_flag, cells))) return rc;
@@ -942,11 +976,11 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
                              cfar ? (uint8_t*)ctx->st_flag.p : nullptr, cfar ? (uint8_t*)ctx->st_flagV.p : nullptr,
                              ctx->stream);
     if (rc) return rc;
-    if (rdm_out && (rc = fetch(ctx, (const float*)ctx->st_rdm.p, rdm_out, batch, P, Ro, out_layout))) return rc;
+    if (rdm_out && (rc = fetch(ctx, (const float*)ctx->st_rdm.p, rdm_out, batch, V, Ro, out_layout))) return rc;
     if (cfar) {
-        if ((rc = fetch(ctx, (const uint8_t*)ctx->st_flag.p, flag_out, batch, P, Ro, out_layout))) return rc;
+        if ((rc = fetch(ctx, (const uint8_t*)ctx->st_flag.p, flag_out, batch, V, Ro, out_layout))) return rc;
         if (flagV_out &&
-            (rc = fetch(ctx, (const uint8_t*)ctx->st_flagV.p, flagV_out, batch, P, Ro, out_layout)))
+            (rc = fetch(ctx, (const uint8_t*)ctx->st_flagV.p, flagV_out, batch, V, Ro, out_layout)))
             return rc;
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

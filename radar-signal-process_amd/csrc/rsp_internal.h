@@ -70,6 +70,9 @@ struct MtdArgs {
     // a frame-contiguous PC buffer.  nwin == 0: CPI j reads rows [j*P, (j+1)*P).
     int nwin;
     int win_start[RSP_MAX_WIN];
+    int pin;             // pulses per CPI and beam (<= P; the FFT zero-pads rows pin..P-1)
+    int beams;           // 2: DMX pair -- RDM = |X_0| + |X_1|, diff (if non-null) = |X_1| - |X_0|
+    float* diff;
     int shift;           // fftshift offset floor(P/2), or 0
     int z_lo, z_hi;      // fun_0v_pressing rows zeroed in the RDM
     const float* win;    // slow-time window, P entries
@@ -98,7 +101,7 @@ struct CfarRArgs {
     int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
 };
 
-bool mtd_size_supported(int P);
+bool mtd_size_supported(int P, int beams = 1);
 bool pc_nfft_supported(int n);
 size_t pc_lds_bytes(int max_nfft);
 

@@ -749,7 +749,10 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums
 // offset is 0 or P/2, a multiple of G, so bin g + G*m lands in row g + G*((m + shift/G) mod E):
 // a wave-uniform rotation, and every row offset is an SGPR operand of the buffer access.
 // REF > 0: Doppler CFAR specialised on the reference window; REF == 0: runtime window.
-template <int P, int REF>
+// P is the Doppler FFT length; a CPI supplies a.pin <= P pulses per beam (rows past pin are
+// the zero padding of fft(x, P, 1): out of the buffer's range, they load as 0).  BEAMS == 2:
+// the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
+template <int P, int REF, int BEAMS>
 __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
@@ -763,22 +766,35 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     const uint32_t R = (uint32_t)a.R_out;
     const int r = blockIdx.x * W + c;
     const bool rv = r < (int)R;
-    const uint32_t plane = (uint32_t)P * R;
+    const uint32_t plane = (uint32_t)P * R;                     // output plane (P Doppler rows)
     const uint32_t cell = (uint32_t)g * R + (uint32_t)r;        // element (g, r) of a plane
-    size_t row0 = cpi * (size_t)P;                               // first PC row of this CPI
-    if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)P + a.win_start[cpi % a.nwin];
-    const auto src = buf_rsrc(pc + row0 * R, plane * 8u);
+    const int pin = a.pin;
+    size_t row0 = cpi * (size_t)pin * BEAMS;                     // first PC row of this CPI
+    if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)pin + a.win_start[cpi % a.nwin];
     const uint32_t vo_in = rv ? cell * 8u : kOob;
     float2 u[E];
+    float m0[BEAMS == 2 ? E : 1];     // |X_0| while beam 1 runs
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        const float2 v = buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u);
-        const float w = a.win[g + G * m];
-        u[m] = make_float2(v.x * w, v.y * w);
+    for (int b = 0; b < BEAMS; ++b) {
+        const auto src = buf_rsrc(pc + (row0 + (size_t)b * pin) * R, (uint32_t)pin * R * 8u);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float2 v = buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u);
+            const float w = a.win[g + G * m];
+            u[m] = make_float2(v.x * w, v.y * w);
+        }
+        fft_reg<P, G, 1, E>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, a.tw);
+        if constexpr (BEAMS == 2) {
+            if (b == 0) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) m0[m] = __builtin_amdgcn_sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
+            }
+        }
     }
-    fft_reg<P, G, 1, E>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, a.tw);
 
     const auto dst = buf_rsrc(rdm + cpi * plane, plane * 4u);
+    const bool want_diff = BEAMS == 2 && a.diff != nullptr;
+    const auto dfr = buf_rsrc(want_diff ? a.diff + cpi * plane : nullptr, want_diff ? plane * 4u : 0u);
     const uint32_t vo_out = rv ? cell * 4u : kOob;
     const int srot = a.shift / G;
     float mg[E];
@@ -788,7 +804,12 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
         if (mm >= E) mm -= E;
         const int v = g + G * mm;
         float x = __builtin_amdgcn_sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
-        if (v >= a.z_lo && v < a.z_hi) x = 0.f;   // fun_0v_pressing
+        if constexpr (BEAMS == 2) {
+            if (want_diff) buf_st_f(x - m0[m], dfr, vo_out, (uint32_t)(G * mm) * R * 4u);   // |R| - |L|
+            x += m0[m];                                                                      // |L| + |R|
+        }
+        // fun_0v_pressing band, or the DMX zeroSetFlagMTD band wrapping through row 0
+        if ((v >= a.z_lo && v < a.z_hi) || v + P < a.z_hi) x = 0.f;
         mg[m] = x;
         buf_st_f(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
@@ -831,23 +852,23 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     }
 }
 
-template <int P, int REF>
+template <int P, int REF, int BEAMS>
 static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                 const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P, REF>,
+        hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P, REF, BEAMS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi), block(kBlock);
-    hipLaunchKernelGGL((mtd_kernel<P, REF>), grid, block, C::lds, s, pc, rdm, flagV, a);
+    hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, C::lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
 
-template <int P>
+template <int P, int BEAMS = 1>
 static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P>;
@@ -856,8 +877,9 @@ static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int
     if (a.shift % C::G != 0 || a.shift < 0 || a.shift >= P) return hipErrorInvalidValue;
     if (a.cv.enabled && a.cv.save + a.cv.ref + 2 > C::SPAD) return hipErrorInvalidValue;
     if ((uint64_t)P * a.R_out * 8 >= (uint64_t)kOob) return hipErrorInvalidValue;
-    if (a.cv.enabled && a.cv.ref == 5) return launch_mtd_pr<P, 5>(pc, rdm, flagV, ncpi, a, s);
-    return launch_mtd_pr<P, 0>(pc, rdm, flagV, ncpi, a, s);
+    if (a.pin < 1 || a.pin > P || a.beams != BEAMS) return hipErrorInvalidValue;
+    if (a.cv.enabled && a.cv.ref == 5) return launch_mtd_pr<P, 5, BEAMS>(pc, rdm, flagV, ncpi, a, s);
+    return launch_mtd_pr<P, 0, BEAMS>(pc, rdm, flagV, ncpi, a, s);
 }
 
 template <int P>
@@ -873,15 +895,17 @@ void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region) {
     switch (P) {
 #define RSP_MR(p) case p: mtd_regions_p<p>(R_out, ncpi, nregions, region); break;
         RSP_MR(16) RSP_MR(32) RSP_MR(64) RSP_MR(128) RSP_MR(256) RSP_MR(512) RSP_MR(1024)
-        RSP_MR(48) RSP_MR(96) RSP_MR(192) RSP_MR(384) RSP_MR(768) RSP_MR(1536)
+        RSP_MR(2048) RSP_MR(48) RSP_MR(96) RSP_MR(192) RSP_MR(384) RSP_MR(768) RSP_MR(1536)
 #undef RSP_MR
         default: break;
     }
 }
 
-bool mtd_size_supported(int P) {
+bool mtd_size_supported(int P, int beams) {
+    if (beams == 2) return P == 512 || P == 1024 || P == 2048;   // the DMX pair (mtd_FFT_num 2048)
+    if (beams != 1) return false;
     switch (P) {
-        case 16: case 32: case 64: case 128: case 256: case 512: case 1024:
+        case 16: case 32: case 64: case 128: case 256: case 512: case 1024: case 2048:
         case 48: case 96: case 192: case 384: case 768: case 1536:
             return true;
         default:
@@ -892,6 +916,14 @@ bool mtd_size_supported(int P) {
 hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
                       hipStream_t s) {
     if (ncpi <= 0) return hipSuccess;
+    if (a.beams == 2) {
+        switch (a.P) {
+            case 512: return launch_mtd_p<512, 2>(pc, rdm, flagV, ncpi, a, s);
+            case 1024: return launch_mtd_p<1024, 2>(pc, rdm, flagV, ncpi, a, s);
+            case 2048: return launch_mtd_p<2048, 2>(pc, rdm, flagV, ncpi, a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (a.P) {
         case 16: return launch_mtd_p<16>(pc, rdm, flagV, ncpi, a, s);
         case 32: return launch_mtd_p<32>(pc, rdm, flagV, ncpi, a, s);
@@ -900,6 +932,7 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
         case 256: return launch_mtd_p<256>(pc, rdm, flagV, ncpi, a, s);
         case 512: return launch_mtd_p<512>(pc, rdm, flagV, ncpi, a, s);
         case 1024: return launch_mtd_p<1024>(pc, rdm, flagV, ncpi, a, s);
+        case 2048: return launch_mtd_p<2048>(pc, rdm, flagV, ncpi, a, s);
         case 48: return launch_mtd_p<48>(pc, rdm, flagV, ncpi, a, s);
         case 96: return launch_mtd_p<96>(pc, rdm, flagV, ncpi, a, s);
         case 192: return launch_mtd_p<192>(pc, rdm, flagV, ncpi, a, s);

@@ -28,7 +28,7 @@ RSP_WIN_KAISER, RSP_WIN_HAMMING, RSP_WIN_RECT = 0, 1, 2
 EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_set_chunk",
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
-           "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev")
+           "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev")
 RSP_NKERNELS = 4
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
 
@@ -52,7 +52,8 @@ class rsp_params(C.Structure):
     _fields_ = [("P", C.c_int64), ("R", C.c_int64), ("R_out", C.c_int64),
                 ("nseg", C.c_int32), ("window", C.c_int32), ("window_beta", C.c_double),
                 ("fftshift", C.c_int32), ("zero_v_div", C.c_int32),
-                ("seg", rsp_pc_segment * RSP_MAX_SEG)]
+                ("seg", rsp_pc_segment * RSP_MAX_SEG),
+                ("mtd_nfft", C.c_int64), ("beams", C.c_int32), ("zero_ends", C.c_int32)]
 
 
 class rsp_cfar_params(C.Structure):
@@ -101,6 +102,8 @@ def load_library(path=None):
     lib.rsp_window_pc_mtd_cfar_dev.restype = C.c_int
     lib.rsp_window_pc_mtd_cfar_dev.argtypes = [vp, vp, i32, i64, i64, i32, C.POINTER(rsp_cfar_params), vp, vp, vp,
                                                vp]
+    lib.rsp_pc_mtd_cfar_diff_dev.restype = C.c_int
+    lib.rsp_pc_mtd_cfar_diff_dev.argtypes = [vp, vp, i32, i64, C.POINTER(rsp_cfar_params), vp, vp, vp, vp, vp]
     lib.rsp_pc_dev.restype = C.c_int
     lib.rsp_pc_dev.argtypes = [vp, vp, i32, i64, vp, vp]
     lib.rsp_create_v2.restype = C.c_int

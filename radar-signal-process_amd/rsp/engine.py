@@ -61,7 +61,8 @@ class Engine:
 
     @property
     def shape(self):
-        return self.spec.P, self.spec.R_out
+        """(Doppler rows, range bins) of one RDM."""
+        return self.spec.V, self.spec.R_out
 
     # ------------------------------------------------------------------ host buffers
     @staticmethod
@@ -96,8 +97,11 @@ class Engine:
         a, dt = self._echo_host(echo, layout)
         shape = a.shape if dt != capi.RSP_C32F16 else a.shape[:-1]
         batch = self._batch_dims(shape, layout)
-        P, Ro = self.spec.P, self.spec.R_out
-        oshape = (batch, P, Ro) if out_layout == capi.RSP_ROWMAJOR else (batch, Ro, P)
+        if batch % self.spec.beams:
+            raise ValueError("a %d-beam context needs echo [batch, %d, P, R]" % (self.spec.beams, self.spec.beams))
+        batch //= self.spec.beams
+        P, Ro, V = self.spec.P, self.spec.R_out, self.spec.V
+        oshape = (batch, V, Ro) if out_layout == capi.RSP_ROWMAJOR else (batch, Ro, V)
         rdm = np.empty(oshape, np.float32)
         flag = flagV = None
         cp = None
@@ -137,36 +141,46 @@ class Engine:
         s = stream if stream is not None else torch.cuda.current_stream()
         return C.c_void_p(s.cuda_stream)
 
-    def run_dev(self, echo, rdm=None, flag=None, flagV=None, cfar=None, stream=None):
-        """echo: torch tensor [batch, P, R] complex64, or [batch, P, R, 2] float16 (I/Q).
-        rdm [batch, P, R_out] float32, flag / flagV uint8 of the same shape (flagV optional).
-        Asynchronous on `stream` (default: torch's current stream)."""
+    def run_dev(self, echo, rdm=None, flag=None, flagV=None, cfar=None, stream=None, diff=None):
+        """echo: torch tensor [batch, P, R] complex64, or [batch, P, R, 2] float16 (I/Q); a
+        two-beam context takes [batch, 2, P, R(, 2)] (beam 0 = left).  rdm [batch, V, R_out]
+        float32, flag / flagV uint8 of the same shape (flagV optional); two beams: rdm is
+        |L| + |R| and diff (optional) |R| - |L|.  Asynchronous on `stream` (default: torch's
+        current stream)."""
         import torch
         if not echo.is_cuda or not echo.is_contiguous():
             raise ValueError("echo must be a contiguous CUDA tensor")
+        nb = self.spec.beams
+        lead = 1 if nb == 1 else 2
         if echo.dtype == torch.complex64:
             dt, batch = capi.RSP_C64, echo.shape[0]
             tail = tuple(echo.shape[1:])
         elif echo.dtype == torch.float16:
             dt, batch = capi.RSP_C32F16, echo.shape[0]
-            tail = tuple(echo.shape[1:3])
+            tail = tuple(echo.shape[1:-1])
             if echo.shape[-1] != 2:
-                raise ValueError("fp16 echo must be [batch, P, R, 2]")
+                raise ValueError("fp16 echo must be [..., P, R, 2]")
         else:
             raise ValueError("echo dtype must be complex64 or float16 I/Q")
-        if tail != (self.spec.P, self.spec.R):
-            raise ValueError("echo is %s, engine expects [batch, %d, %d]" % (tuple(echo.shape), self.spec.P, self.spec.R))
-        want = (batch, self.spec.P, self.spec.R_out)
-        for t, dtp in ((rdm, torch.float32), (flag, torch.uint8), (flagV, torch.uint8)):
+        want_in = (self.spec.P, self.spec.R) if lead == 1 else (nb, self.spec.P, self.spec.R)
+        if tail != want_in:
+            raise ValueError("echo is %s, engine expects [batch, %s]" % (tuple(echo.shape), want_in))
+        want = (batch, self.spec.V, self.spec.R_out)
+        for t, dtp in ((rdm, torch.float32), (flag, torch.uint8), (flagV, torch.uint8), (diff, torch.float32)):
             if t is not None and (tuple(t.shape) != want or t.dtype != dtp or not t.is_contiguous() or not t.is_cuda):
                 raise ValueError("output tensor must be contiguous CUDA %s of shape %s" % (dtp, want))
+        if diff is not None and nb != 2:
+            raise ValueError("diff output needs a two-beam context")
         cp = cfar.to_c() if cfar is not None else None
-        rc = self.lib.rsp_pc_mtd_cfar_dev(
-            self.ctx, C.c_void_p(echo.data_ptr()), dt, batch, C.byref(cp) if cp is not None else None,
-            C.c_void_p(rdm.data_ptr()) if rdm is not None else None,
-            C.c_void_p(flag.data_ptr()) if flag is not None else None,
-            C.c_void_p(flagV.data_ptr()) if flagV is not None else None,
-            self._stream_handle(stream))
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None   # noqa: E731
+        if nb == 2:
+            rc = self.lib.rsp_pc_mtd_cfar_diff_dev(
+                self.ctx, C.c_void_p(echo.data_ptr()), dt, batch, C.byref(cp) if cp is not None else None,
+                ptr(rdm), ptr(diff), ptr(flag), ptr(flagV), self._stream_handle(stream))
+        else:
+            rc = self.lib.rsp_pc_mtd_cfar_dev(
+                self.ctx, C.c_void_p(echo.data_ptr()), dt, batch, C.byref(cp) if cp is not None else None,
+                ptr(rdm), ptr(flag), ptr(flagV), self._stream_handle(stream))
         capi.check(rc, self.ctx)
 
     def window_dev(self, frames, win, rdm=None, flag=None, flagV=None, cfar=None, stream=None):

@@ -103,6 +103,14 @@ class Spec:
     zero_v_div: int = 150
     cfar_segments: list = field(default_factory=list)   # 0-based [lo, hi)
     radar: dict = field(default_factory=dict)
+    mtd_nfft: int = 0          # Doppler FFT length V (0 = P); DMX: 2048 over 1536 pulses
+    beams: int = 1             # 2: DMX left/right pair, RDM = |X_L| + |X_R|
+    zero_ends: int = 0         # DMX zeroSetFlagMTD: MTD_0_num + 1 (0 = fun_0v_pressing instead)
+
+    @property
+    def V(self):
+        """Doppler rows of the RDM."""
+        return self.mtd_nfft or self.P
 
     def to_c(self):
         """Build the ctypes rsp_params; returns (struct, keepalive list)."""
@@ -111,6 +119,7 @@ class Spec:
         prm.nseg = len(self.segments)
         prm.window, prm.window_beta = self.window, self.window_beta
         prm.fftshift, prm.zero_v_div = self.fftshift, self.zero_v_div
+        prm.mtd_nfft, prm.beams, prm.zero_ends = self.mtd_nfft, self.beams, self.zero_ends
         keep = []
         for i, s in enumerate(self.segments):
             g = prm.seg[i]
@@ -193,12 +202,49 @@ def dmx(P=128, R=4096, radar=None):
     return Spec("dmx", P, R, R, segs, cfar_segments=[(0, R)], radar=rp)
 
 
-PRESETS = {"v2": v2, "legacy": legacy, "dmx": dmx}
+# DMX_SignalProcessing_main_xzr.m waveform 1 (:100-120): fs 12.5 MHz, PRT 52.08 us, 62 short +
+# 504 long samples, FFT_num 512, mtd_FFT_num 2048, prtNum 1536; carrier from freValueGen.m
+DMX_FS = 12.5e6
+DMX_PRT = 52.08e-6
+DMX_FC = 9365e6            # freValueGen(0 or 1)
+
+
+def dmx_native(P=1536, R=566, point_short=62, fft_num=512, mtd_fft_num=2048, fc=DMX_FC, mtd_v=1.0):
+    """The DMX chain at its native sizes (DMX_SignalProcessing_main_xzr.m:146,202,208-229,
+    331-353,414-426,462-465): short part = filter(b_raw, 1, x) with the raw integer taps (no
+    scale, no shift); long part = ifft(fft(x, 512) .* conj(fft(ref.*kaiser(67,4.5), 512)))
+    (circular, 512 outputs); slow time = fft(pc .* hamming(P), 2048, 1) without fftshift for
+    the left and right beams, RDM = |L| + |R|; rows 1:M0+1 and 2048-M0+1:2048 zeroed."""
+    long_in = R - point_short
+    if long_in > fft_num:
+        raise ValueError("long part (%d) exceeds FFT_num %d" % (long_in, fft_num))
+    R_out = point_short + fft_num
+    segs = [Segment(capi.RSP_SEG_FIR, 0, point_short, 0, point_short, FIR_TAPS.astype(np.float64)),
+            Segment(capi.RSP_SEG_MF, point_short, long_in, point_short, fft_num, dmx_replica(), nfft=fft_num)]
+    prf = 1.0 / DMX_PRT
+    wl = C_LIGHT / fc
+    delta_v = wl * (prf / mtd_fft_num) / 2.0                      # :322-323
+    m0 = int(math.floor(mtd_v / delta_v))                         # MTD_0_num (:462)
+    rp = dict(prtNum=P, fs=DMX_FS, fc=fc, prt=DMX_PRT, prf=prf, wavelength=wl, mtd_v=mtd_v, M0=m0)
+    return Spec("dmx_native", P, R, R_out, segs, window=capi.RSP_WIN_HAMMING, fftshift=0, zero_v_div=0,
+                cfar_segments=[(0, point_short), (point_short, R_out)], radar=rp,
+                mtd_nfft=mtd_fft_num, beams=2, zero_ends=m0 + 1)
+
+
+def dmx_native_cfar(spec, T=7.0):
+    """The DMX CFAR settings (:235-247): ref 5, guard 7, T 7, GO, range stage on; M0 =
+    MTD_0_num; no /20 suppression (the zeroed rows are the stripped ones)."""
+    return Cfar(TR=T, TV=T, M0=spec.radar["M0"], zero_v_div=0, segments=list(spec.cfar_segments))
+
+
+PRESETS = {"v2": v2, "legacy": legacy, "dmx": dmx, "dmx_native": dmx_native}
 
 
 def make(name, P, R):
     if name == "legacy":
         return legacy(P, R)
+    if name == "dmx_native":
+        return dmx_native(P, R)
     return PRESETS[name](P, R)
 
 
@@ -242,6 +288,8 @@ class Cfar:
 
 
 def default_cfar(spec, T=5.0, mtd_v=3.0, zero_v_div=20):
+    if spec.name == "dmx_native":
+        return dmx_native_cfar(spec)
     rp = spec.radar
     M0 = mtd_zero_num(spec.P, rp["wavelength"], rp["prf"], mtd_v)
     return Cfar(TR=T, TV=T, M0=M0, zero_v_div=zero_v_div, segments=list(spec.cfar_segments))

@@ -158,3 +158,56 @@ def test_chain_rflag0_is_flagV(torch_cuda):
     hard, soft = flag_mismatch(f.cpu().numpy(), flag, amb)
     assert hard == 0 and soft <= 2
     eng.close()
+
+
+def test_dmx_native_two_beam_parity(torch_cuda):
+    """Row a8: the DMX chain at native size (1536 PRTs x 566 samples, two beams): PC (raw FIR
+    short part + circular 512-point MF), fft(pc.*hamming, 2048, 1), |L|+|R| with the
+    zeroSetFlagMTD rows, |R|-|L|, executeCFAR per short/long part on the sum.  Bars: sum
+    rel-err <= 1e-5; diff error <= 1e-5 of the sum's norm (it is a difference of magnitudes);
+    flags exact outside the near-threshold band."""
+    torch = torch_cuda
+    import rsp_ref as ref
+    from rsp import presets
+    from rsp.engine import Engine
+    spec = presets.dmx_native()
+    assert spec.R_out == 574 and spec.V == 2048 and spec.radar["M0"] == 6
+    eng = Engine(spec, device=0)
+    cf = presets.default_cfar(spec)
+    batch = 2
+    rng = np.random.default_rng(1008)
+    e = (rng.standard_normal((batch, 2, spec.P, spec.R)) + 1j * rng.standard_normal((batch, 2, spec.P, spec.R))) \
+        * np.sqrt(0.5)
+    # moving targets in both beams (different gains): the replica itself, delayed into the
+    # long part, with a per-PRT Doppler phase -- it compresses to a range/Doppler peak
+    rep = presets.load_data("refDDCDataMF1").astype(np.complex128).ravel()
+    m = np.arange(spec.P)[:, None]
+    for delay, fd, amp in ((150, 0.11, 0.5), (320, -0.23, 0.3)):
+        sig = amp * np.exp(2j * np.pi * fd * m) * rep[None, :] / np.abs(rep).max()
+        c0 = 62 + delay
+        e[:, 0, :, c0:c0 + rep.size] += sig
+        e[:, 1, :, c0:c0 + rep.size] += 0.6 * sig
+    e = e.astype(np.complex64)
+    d_in = torch.from_numpy(e).cuda()
+    shp = (batch, spec.V, spec.R_out)
+    d_sum = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_diff = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.run_dev(d_in, rdm=d_sum, diff=d_diff, flag=d_flag, cfar=cf)
+    torch.cuda.synchronize()
+    H = ref.dmx_matched_filter(presets.load_data("refDDCDataMF1"), 512)
+    sums, diffs = [], []
+    for b in range(batch):
+        pcl = ref.dmx_pulse_compression(e[b, 0].astype(np.complex128), 62, 512, H)
+        pcr = ref.dmx_pulse_compression(e[b, 1].astype(np.complex128), 62, 512, H)
+        s, d = ref.dmx_mtd_pair(pcl, pcr, 2048, spec.radar["M0"])
+        sums.append(s)
+        diffs.append(d)
+    s_ref, d_ref = np.stack(sums), np.stack(diffs)
+    assert rel_err(d_sum.cpu().numpy(), s_ref) < RDM_TOL
+    assert np.linalg.norm(d_diff.cpu().numpy() - d_ref) / np.linalg.norm(s_ref) < RDM_TOL
+    flag, _, amb = oracle_flags(s_ref, cf)
+    hard, soft = flag_mismatch(d_flag.cpu().numpy(), flag, amb)
+    assert hard == 0 and soft <= 2, (hard, soft)
+    assert flag.sum() > 0
+    eng.close()

@@ -140,3 +140,21 @@ def test_c_oracle_matches_numpy_oracle(name, P, R):
         np.testing.assert_array_equal(fc[i], f)
         np.testing.assert_array_equal(fvc[i], fv)
     assert fc.sum() > 0
+
+
+def test_dmx_mtd_pair_matches_generic_mtd():
+    """dmx_mtd_pair = the generic fun_Process_MTD restatement with hamming, nfft 2048 and no
+    shift, summed over the beams; the zeroSetFlagMTD rows are 1:M0+1 and end-M0+1:end."""
+    rng = np.random.default_rng(3)
+    P, R, nfft, m0 = 96, 5, 256, 4
+    pl = rng.standard_normal((P, R)) + 1j * rng.standard_normal((P, R))
+    pr = rng.standard_normal((P, R)) + 1j * rng.standard_normal((P, R))
+    s, d = ref.dmx_mtd_pair(pl, pr, nfft, m0)
+    ml = ref.fun_Process_MTD(pl, window=ref.hamming(P), nfft=nfft, shift=False)
+    mr = ref.fun_Process_MTD(pr, window=ref.hamming(P), nfft=nfft, shift=False)
+    np.testing.assert_allclose(d, mr - ml, rtol=0, atol=1e-9)
+    keep = np.ones(nfft, bool)
+    keep[:m0 + 1] = False
+    keep[nfft - m0:] = False
+    np.testing.assert_allclose(s[keep], (ml + mr)[keep], rtol=0, atol=1e-9)
+    assert not s[~keep].any() and keep.sum() == nfft - 2 * m0 - 1
