@@ -247,10 +247,13 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     if (beams < 1 || beams > 2) return fail(nullptr, RSP_ERR_ARG, "rsp_create: beams=%d (1 or 2)", p.beams);
     if (V < p.P)
         return fail(nullptr, RSP_ERR_SHAPE, "rsp_create: mtd_nfft=%lld < P=%lld", (long long)V, (long long)p.P);
-    if (!rsp::mtd_size_supported((int)V, beams))
+    const bool bluestein = !rsp::mtd_size_supported((int)V, beams) && beams == 1 && V == p.P &&
+                           rsp::mtd_bluestein_nf((int)V) > 0;
+    if (!rsp::mtd_size_supported((int)V, beams) && !bluestein)
         return fail(nullptr, RSP_ERR_UNSUPPORTED,
-                    "rsp_create: Doppler length %lld (beams %d) not built (2^k or 3*2^k, 16..2048; two beams: "
-                    "512, 1024, 2048)", (long long)V, beams);
+                    "rsp_create: Doppler length %lld (beams %d) not built (radix plans 2^k, 3*2^k up to 2048; "
+                    "other even and odd P <= 1024 by Bluestein; two beams: 512, 1024, 2048)",
+                    (long long)V, beams);
     if (p.zero_ends < 0 || 2 * (int64_t)p.zero_ends > V)
         return fail(nullptr, RSP_ERR_ARG, "rsp_create: zero_ends=%d out of range", p.zero_ends);
     if (p.nseg < 0 || p.nseg > RSP_MAX_SEG)
@@ -434,7 +437,36 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     int rc = upload(ctx, wf, &dw);
     if (rc) return bail(rc);
     m.win = dw;
-    rc = twiddles(ctx, (int)V, &m.tw);
+    if (bluestein) {
+        // X[k] = c[k] sum_n (x[n] w[n] c[n]) conj(c[k-n]), c[n] = exp(-j pi n^2 / V): tables in
+        // fp64 (n^2 reduced mod 2V so the phase stays exact), the chirp spectrum by FFT
+        const int nf = rsp::mtd_bluestein_nf((int)V);
+        auto chirp = [&](int64_t n) {
+            const double ph = -M_PI * (double)((n * n) % (2 * V)) / (double)V;
+            return cd(std::cos(ph), std::sin(ph));
+        };
+        std::vector<float2> bwc((size_t)nf, float2{0.f, 0.f}), bsp((size_t)nf);
+        for (int64_t n = 0; n < V; ++n) {
+            const cd z = w[(size_t)n] * chirp(n);
+            bwc[(size_t)n] = float2{(float)z.real(), (float)z.imag()};
+        }
+        std::vector<cd> b((size_t)nf, cd(0, 0));
+        for (int64_t n = 0; n < V; ++n) {
+            b[(size_t)n] = std::conj(chirp(n));
+            if (n) b[(size_t)(nf - n)] = std::conj(chirp(n));
+        }
+        fft_pow2(b);
+        for (int i = 0; i < nf; ++i) bsp[(size_t)i] = float2{(float)(b[(size_t)i].real() / nf), (float)(b[(size_t)i].imag() / nf)};
+        float2 *dbwc = nullptr, *dbsp = nullptr;
+        if ((rc = upload(ctx, bwc, &dbwc))) return bail(rc);
+        if ((rc = upload(ctx, bsp, &dbsp))) return bail(rc);
+        m.bnf = nf;
+        m.bwc = dbwc;
+        m.bspec = dbsp;
+        rc = twiddles(ctx, nf, &m.tw);
+    } else {
+        rc = twiddles(ctx, (int)V, &m.tw);
+    }
     if (rc) return bail(rc);
     *out = ctx;
     return RSP_OK;

@@ -73,6 +73,12 @@ struct MtdArgs {
     int pin;             // pulses per CPI and beam (<= P; the FFT zero-pads rows pin..P-1)
     int beams;           // 2: DMX pair -- RDM = |X_0| + |X_1|, diff (if non-null) = |X_1| - |X_0|
     float* diff;
+    // Bluestein plan for P without a radix plan (v2 native P = 332): bnf > 0 is the power-of-
+    // two convolution length, bwc[n] = w[n] exp(-j pi n^2/P) (0 for n >= P), bspec = FFT of the
+    // conjugate chirp / bnf; tw is then the bnf-point twiddle table.
+    int bnf;
+    const float2* bwc;
+    const float2* bspec;
     int shift;           // fftshift offset floor(P/2), or 0
     int z_lo, z_hi;      // fun_0v_pressing rows zeroed in the RDM
     const float* win;    // slow-time window, P entries
@@ -126,6 +132,8 @@ hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hit
                             int nregions, int region, const CfarRArgs& a, hipStream_t s);
 // MTD workgroups per launch and cells per workgroup (hit-list regions)
 void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region);
+// Bluestein convolution length for a P without a radix plan (0: unsupported)
+int mtd_bluestein_nf(int P);
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
                          const CfarRArgs& a, hipStream_t s);
 // dtype/layout conversion of a host-API input into [batch][P][R] complex float32.

@@ -852,6 +852,113 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     }
 }
 
+// Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
+// MTD/main_produce_dataset_win_xzr_v2.m:31) by Bluestein's identity:
+//   X[k] = c[k] sum_n (x[n] w[n] c[n]) conj(c[k-n]),   c[n] = exp(-j pi n^2 / P),
+// a circular convolution of length NF >= 2P - 1 (power of two): FFT, multiply by the chirp's
+// spectrum, FFT again (the inverse as conj(FFT(conj))).  |c[k]| = 1, so the magnitude
+// needs no final chirp.  Bins k < P are kept; fftshift / 0-v / Doppler CFAR as mtd_kernel
+// (runtime CFAR window), with per-element row offsets (P is not a multiple of G).
+template <int NF>
+__global__ __launch_bounds__(kBlock) void mtd_bluestein_kernel(const float2* __restrict__ pc,
+                                                               float* __restrict__ rdm,
+                                                               uint8_t* __restrict__ flagV, MtdArgs a) {
+    using C = MtdCfg<NF>;
+    constexpr int G = C::G, E = C::E, W = C::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_hits;
+    if (threadIdx.x == 0) s_hits = 0u;
+    const int c = threadIdx.x % W, g = threadIdx.x / W;
+    const size_t cpi = blockIdx.y;
+    const uint32_t R = (uint32_t)a.R_out;
+    const int r = blockIdx.x * W + c;
+    const bool rv = r < (int)R;
+    const int P = a.pin;
+    const uint32_t plane = (uint32_t)P * R;
+    size_t row0 = cpi * (size_t)P;
+    if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)P + a.win_start[cpi % a.nwin];
+    const auto src = buf_rsrc(pc + row0 * R, plane * 8u);           // rows >= P load as 0
+    const uint32_t vo_in = rv ? ((uint32_t)g * R + (uint32_t)r) * 8u : kOob;
+    float2 u[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m)
+        u[m] = cmul(buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u), a.bwc[g + G * m]);
+    float2* slot = reinterpret_cast<float2*>(smem) + c * C::SLOT;
+    fft_reg<NF, G, 1, E>(u, slot, g, a.tw);
+#pragma unroll
+    for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], a.bspec[g + G * m]);   // conj(A .* B), 1/NF in B
+    fft_reg<NF, G, 1, E>(u, slot, g, a.tw);                                  // conj of the convolution
+
+    const auto dst = buf_rsrc(rdm + cpi * plane, plane * 4u);
+    float mg[E];
+    int vr[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = g + G * m;                   // Doppler bin
+        int v = k + a.shift;                       // fftshift: out[v] = X[(v - shift) mod P]
+        if (v >= P) v -= P;
+        float x = __builtin_amdgcn_sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
+        if (v >= a.z_lo && v < a.z_hi) x = 0.f;   // fun_0v_pressing
+        mg[m] = x;
+        vr[m] = k < P ? v : -1;
+        if (k < P) buf_st_f(x, dst, rv ? ((uint32_t)v * R + (uint32_t)r) * 4u : kOob, 0u);
+    }
+    if (!a.cv.enabled) return;
+    __syncthreads();  // the FFT exchange slots are free from here on
+    float* mag = reinterpret_cast<float*>(smem) + c * C::MS;
+#pragma unroll
+    for (int m = 0; m < E; ++m)
+        if (vr[m] >= 0) mag[vr[m]] = (vr[m] >= a.cv.cz_lo && vr[m] < a.cv.cz_hi) ? 0.f : mg[m];
+    __syncthreads();
+    const int v0 = g * E, v1 = v0 + E < P ? v0 + E : P;    // this thread's run of Doppler rows
+    const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
+    DopplerOut o;
+    o.want_fv = flagV != nullptr;
+    o.fused = a.flag != nullptr;
+    o.rflag = a.rflag != 0;
+    o.fv = buf_rsrc(o.want_fv ? flagV + cpi * plane : nullptr, o.want_fv ? plane : 0u);
+    o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
+    o.vo = (rv && v0 < P) ? (uint32_t)v0 * R + (uint32_t)r : kOob;
+    o.R = R;
+    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+    o.hits = a.hits ? a.hits + (size_t)wg * ((size_t)W * P) : nullptr;
+    o.lds_count = &s_hits;
+    o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
+    float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
+    doppler_sums(mag, sums, P, a.cv.ref, v0, v1);
+    __syncthreads();
+    doppler_flags(mag, sums, a.cv, col_on, v0, v1, o);
+    if (o.fused && o.rflag) {
+        __syncthreads();
+        if (threadIdx.x == 0) a.hit_count[wg] = s_hits;
+    }
+}
+
+template <int NF>
+static hipError_t launch_mtd_bluestein(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
+                                       hipStream_t s) {
+    using C = MtdCfg<NF>;
+    if (a.pin < 2 || 2 * a.pin - 1 > NF || a.beams != 1 || a.shift < 0 || a.shift >= a.pin) return hipErrorInvalidValue;
+    if (a.cv.enabled && a.cv.save + a.cv.ref + 2 > C::SPAD) return hipErrorInvalidValue;
+    if ((uint64_t)a.pin * a.R_out * 8 >= (uint64_t)kOob) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)mtd_bluestein_kernel<NF>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi), block(kBlock);
+    hipLaunchKernelGGL((mtd_bluestein_kernel<NF>), grid, block, C::lds, s, pc, rdm, flagV, a);
+    return hipGetLastError();
+}
+
+int mtd_bluestein_nf(int P) {
+    int nf = 64;
+    while (nf < 2 * P - 1) nf <<= 1;
+    return nf <= 2048 ? nf : 0;
+}
+
 template <int P, int REF, int BEAMS>
 static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                 const MtdArgs& a, hipStream_t s) {
@@ -892,6 +999,14 @@ static void mtd_regions_p(int R_out, int ncpi, int* nregions, int* region) {
 void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region) {
     *nregions = 0;
     *region = 0;
+    if (!mtd_size_supported(P, 1)) {   // Bluestein: NF-point tiles, P rows kept
+        const int nf = mtd_bluestein_nf(P);
+        if (!nf) return;
+        const int W = kBlock / (nf / 16);
+        *nregions = ((R_out + W - 1) / W) * ncpi;
+        *region = W * P;
+        return;
+    }
     switch (P) {
 #define RSP_MR(p) case p: mtd_regions_p<p>(R_out, ncpi, nregions, region); break;
         RSP_MR(16) RSP_MR(32) RSP_MR(64) RSP_MR(128) RSP_MR(256) RSP_MR(512) RSP_MR(1024)
@@ -916,6 +1031,17 @@ bool mtd_size_supported(int P, int beams) {
 hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
                       hipStream_t s) {
     if (ncpi <= 0) return hipSuccess;
+    if (a.bnf > 0) {
+        switch (a.bnf) {
+            case 64: return launch_mtd_bluestein<64>(pc, rdm, flagV, ncpi, a, s);
+            case 128: return launch_mtd_bluestein<128>(pc, rdm, flagV, ncpi, a, s);
+            case 256: return launch_mtd_bluestein<256>(pc, rdm, flagV, ncpi, a, s);
+            case 512: return launch_mtd_bluestein<512>(pc, rdm, flagV, ncpi, a, s);
+            case 1024: return launch_mtd_bluestein<1024>(pc, rdm, flagV, ncpi, a, s);
+            case 2048: return launch_mtd_bluestein<2048>(pc, rdm, flagV, ncpi, a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (a.beams == 2) {
         switch (a.P) {
             case 512: return launch_mtd_p<512, 2>(pc, rdm, flagV, ncpi, a, s);

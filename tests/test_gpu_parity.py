@@ -233,8 +233,8 @@ def test_error_behaviour(torch_cuda):
     with pytest.raises(RspError) as ei:
         eng.pc_mtd_cfar(_echo(eng, 1), cf)
     assert ei.value.code == capi.RSP_ERR_CFAR_WINDOW
-    with pytest.raises(RspError) as ei:      # unsupported Doppler FFT length
-        Engine(presets.v2(100, 1024))
+    with pytest.raises(RspError) as ei:      # no radix plan and beyond the Bluestein range
+        Engine(presets.v2(1100, 1024))
     assert ei.value.code == capi.RSP_ERR_UNSUPPORTED
 
 
