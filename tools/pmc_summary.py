@@ -14,10 +14,18 @@ import os
 import sys
 
 
+# kernel-name fragment -> the bench's kernel label (rsp_profile ids)
+LABELS = (("pc_persist_kernel", "pc_kernel"), ("pc_mf_kernel", "pc_kernel"), ("pc_kernel", "pc_kernel"),
+          ("mtd_bluestein_kernel", "mtd_kernel"), ("mtd_kernel", "mtd_kernel"),
+          ("cfar_hits_kernel", "cfar_r_kernel"), ("cfar_r16_kernel", "cfar_r_kernel"),
+          ("cfar_r_kernel", "cfar_r_kernel"), ("cfar_r_generic_kernel", "cfar_r_kernel"),
+          ("cfar_v_kernel", "cfar_v_kernel"), ("fillBuffer", "flag_memset"))
+
+
 def short(name):
-    for k in ("pc_mf_kernel", "pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "cfar_fused"):
+    for k, label in LABELS:
         if k in name:
-            return k
+            return label
     return name[:40]
 
 
@@ -39,7 +47,7 @@ def main():
     acc, dur = load(pmc_dir)
     rows = {}
     for k, cs in acc.items():
-        if not any(x in k for x in ("pc_", "mtd", "cfar")):
+        if not any(x in k for x in ("pc_", "mtd", "cfar", "memset")):
             continue
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         d = sum(dur[k]) / len(dur[k]) if dur[k] else float("nan")
@@ -76,7 +84,7 @@ def main():
         # bench.py reads kernels[<name>].hbm_bytes_per_launch as roofline.traffic
         out = args[args.index("--json") + 1]
         cpl = int(args[args.index("--cpis-per-launch") + 1]) if "--cpis-per-launch" in args else None
-        names = {"pc_mf_kernel": "pc_kernel", "pc_kernel": "pc_kernel"}
+        names = {}
         doc = {"note": "rocprofv3 --pmc, one counter group per pass; HBM-side bytes per launch = "
                        "2*FETCH_SIZE*1024 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM) + "
                        "WRITE_SIZE*1024; Infinity-Cache hits are counted by these counters",
