@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
-    ap.add_argument("--profile-every", type=int, default=8, help="bracket every N-th kernel launch with events")
+    ap.add_argument("--profile-every", type=int, default=7,
+                    help="bracket every N-th kernel launch with events (coprime with the 2-3 launches per chunk)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.P = args.P or cfg["P"]

@@ -194,6 +194,12 @@ int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t
                  const rsp_cfar_params* cfar, uint8_t* d_flag, uint8_t* d_flagV,
                  void* stream);
 
+/* The chain after pulse compression (fun_Process_MTD + fun_0v_pressing + executeCFAR) on
+ * already pulse-compressed rows, e.g. from rsp_pc_dev: d_pc [batch][beams][P][R_out] RSP_C64.
+ * Outputs as rsp_pc_mtd_cfar_dev. */
+int rsp_mtd_cfar_dev(rsp_ctx* ctx, const void* d_pc, int64_t batch, const rsp_cfar_params* cfar,
+                     float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV, void* stream);
+
 /* rsp_pc_mtd_cfar_dev for a two-beam context (rsp_params.beams == 2): d_echo
  * [batch][2][P][R]; d_sum [batch][V][R_out] = |X_L| + |X_R| (the RDM, zeroSetFlagMTD
  * applied); d_diff (nullable) = |X_R| - |X_L|; CFAR runs on the sum

@@ -736,7 +736,7 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
 // frames plus the look-ahead frame once, and every window reads its rows from that PC.
 static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
                      const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                     float* d_diff, hipStream_t s) {
+                     float* d_diff, hipStream_t s, bool pc_input = false) {
     const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out, V = ctx->V, NB = ctx->beams;
     const size_t esz = dtype == RSP_C64 ? 8 : 4;
     rsp::MtdArgs m = ctx->mtd;
@@ -761,23 +761,27 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
     const size_t plane = (size_t)V * Ro;                  // output cells per CPI
     const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
     const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * NB * P;
-    int rc = ensure(ctx, ctx->scratch_pc, (size_t)ns * pcrows * Ro * sizeof(float2));
+    int rc = pc_input ? RSP_OK : ensure(ctx, ctx->scratch_pc, (size_t)ns * pcrows * Ro * sizeof(float2));
     if (rc) return rc;
     int nreg = 0, reg = 0;
     if (cfar) {
         // fused range stage: per-lane hit lists, one region per MTD workgroup sized to its
         // cells (no overflow, no global atomics), and per-workgroup counts
         if (cells > 0xffffffffull) return fail(ctx, RSP_ERR_UNSUPPORTED, "chunk too large for 32-bit hit indices");
+        // two slots per lane: chunk k's list is read by the next MTD launch on its lane while
+        // that launch fills the other slot
         rsp::mtd_regions((int)V, (int)Ro, (int)(cu * ocpi), &nreg, &reg);
-        rc = ensure(ctx, ctx->hit_list, (size_t)ns * nreg * reg * sizeof(uint32_t));
+        rc = ensure(ctx, ctx->hit_list, (size_t)2 * ns * nreg * reg * sizeof(uint32_t));
         if (rc) return rc;
-        rc = ensure(ctx, ctx->hit_ctr, (size_t)ns * nreg * sizeof(uint32_t));
-        if (rc) return rc;
-    }
-    if (!d_rdm) {
-        rc = ensure(ctx, ctx->tmp_rdm, (size_t)ns * cells * sizeof(float));
+        rc = ensure(ctx, ctx->hit_ctr, (size_t)2 * ns * nreg * sizeof(uint32_t));
         if (rc) return rc;
     }
+    if (!d_rdm) {   // internal RDM: two slots per lane for the same reason
+        rc = ensure(ctx, ctx->tmp_rdm, (size_t)2 * ns * cells * sizeof(float));
+        if (rc) return rc;
+    }
+    if (cfar && cr.rflag)   // background of the whole flag output; the range stage writes the 1s
+        HIP_TRY(ctx, hipMemsetAsync(d_flag, 0, (size_t)units * ocpi * plane, s));
     // Chunk k runs on lane k % ns (lane 0 = the caller's stream), each lane with its own
     // scratch slot, so PC of one chunk overlaps MTD / CFAR of the previous one.  The lanes
     // fork from and join back into the caller's stream.
@@ -792,35 +796,67 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
             HIP_TRY(ctx, hipStreamWaitEvent(lanes[i], ctx->ev_fork, 0));
         }
     }
+    // A chunk's range stage (its hit list) runs inside the next MTD launch on its lane, so the
+    // lane timeline carries no separate small kernel; a lane's last chunk gets its own launch.
+    struct Pending {
+        int nreg = 0, reg = 0;
+        const float* rdm = nullptr;
+        uint8_t* flag = nullptr;
+        const uint32_t* hits = nullptr;
+        const uint32_t* counts = nullptr;
+    } pend[4];
     for (int64_t k = 0; k < nchunks; ++k) {
         const int64_t u0 = k * cu;
         const int64_t n = units - u0 < cu ? units - u0 : cu;
         const int64_t ncpi = n * ocpi;                     // CPIs this chunk produces
         const size_t o0 = (size_t)u0 * ocpi * plane;      // output offset
         const int lane = (int)(k % ns);
+        const int slot = lane * 2 + (int)((k / ns) & 1);   // double-buffered per lane
         hipStream_t ls = lanes[lane];
         const char* ein = (const char*)d_echo + (size_t)u0 * NB * P * R * esz;
-        float* rdm = d_rdm ? d_rdm + o0 : (float*)ctx->tmp_rdm.p + lane * cells;
+        float* rdm = d_rdm ? d_rdm + o0 : (float*)ctx->tmp_rdm.p + slot * cells;
         uint8_t* fv = (cfar && d_flagV) ? d_flagV + o0 : nullptr;
-        float2* pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
-        HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls));
+        float2* pcs;
+        if (pc_input) {   // d_echo already holds pulse-compressed rows [units][beams][P][R_out]
+            pcs = (float2*)d_echo + (size_t)u0 * NB * P * Ro;
+        } else {
+            pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
+            HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls));
+        }
         m.diff = d_diff ? d_diff + o0 : nullptr;
+        m.prev_nregions = 0;
         if (cfar) {
             m.flag = d_flag + o0;
             m.rflag = cr.rflag;
-            m.hits = (uint32_t*)ctx->hit_list.p + (size_t)lane * nreg * reg;
-            m.hit_count = (uint32_t*)ctx->hit_ctr.p + (size_t)lane * nreg;
+            m.hits = (uint32_t*)ctx->hit_list.p + (size_t)slot * nreg * reg;
+            m.hit_count = (uint32_t*)ctx->hit_ctr.p + (size_t)slot * nreg;
+            const Pending& pv = pend[lane];
+            if (pv.nreg > 0) {
+                m.prev_rdm = pv.rdm;
+                m.prev_flag = pv.flag;
+                m.prev_hits = pv.hits;
+                m.prev_count = pv.counts;
+                m.prev_nregions = pv.nreg;
+                m.prev_region = pv.reg;
+                m.prev_cr = cr;
+            }
         }
-        if (cfar && cr.rflag)   // background of the flag plane; the range stage writes the 1s
-            HIP_TRY(ctx, hipMemsetAsync(m.flag, 0, (size_t)ncpi * plane, ls));
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
-            int nr = 0, rg = 0;
-            rsp::mtd_regions((int)V, (int)Ro, (int)ncpi, &nr, &rg);   // this chunk's workgroups
-            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] {
-                return rsp::launch_cfar_hits(rdm, m.flag, m.hits, m.hit_count, nr, rg, cr, ls);
-            }));
+            Pending& pv = pend[lane];
+            rsp::mtd_regions((int)V, (int)Ro, (int)ncpi, &pv.nreg, &pv.reg);   // this chunk's workgroups
+            pv.rdm = rdm;
+            pv.flag = m.flag;
+            pv.hits = m.hits;
+            pv.counts = m.hit_count;
         }
+    }
+    for (int lane = 0; lane < ns; ++lane) {   // each lane's last chunk
+        const Pending& pv = pend[lane];
+        if (pv.nreg > 0)
+            HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, lanes[lane], [&] {
+                return rsp::launch_cfar_hits(pv.rdm, pv.flag, pv.hits, pv.counts, pv.nreg, pv.reg, cr, lanes[lane]);
+            }));
     }
     for (int i = 1; i < ns; ++i) {
         HIP_TRY(ctx, hipEventRecord(ctx->ev_join[i - 1], lanes[i]));
@@ -849,6 +885,15 @@ int rsp_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t
     if (batch == 0) return RSP_OK;
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
     return run_chain(ctx, d_echo, dtype, batch, 0, cfar, d_rdm, d_flag, d_flagV, nullptr, (hipStream_t)stream);
+}
+
+int rsp_mtd_cfar_dev(rsp_ctx* ctx, const void* d_pc, int64_t batch, const rsp_cfar_params* cfar, float* d_rdm,
+                     uint8_t* d_flag, uint8_t* d_flagV, void* stream) {
+    int rc = check_chain_args(ctx, "rsp_mtd_cfar_dev", d_pc, RSP_C64, batch, cfar, d_rdm, d_flag);
+    if (rc) return rc;
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    return run_chain(ctx, d_pc, RSP_C64, batch, 0, cfar, d_rdm, d_flag, d_flagV, nullptr, (hipStream_t)stream, true);
 }
 
 int rsp_pc_mtd_cfar_diff_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch,

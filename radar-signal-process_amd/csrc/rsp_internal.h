@@ -61,6 +61,19 @@ struct CfarVArgs {
     int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
 };
 
+// Range-dimension CFAR at the Doppler hits (executeCFAR.m:35-89).
+struct CfarRArgs {
+    int V, R;
+    int lo, hi;          // used rows
+    int rflag;
+    int ref, save, method;
+    float T;
+    float Tr;            // T / ref
+    int cz_lo, cz_hi;    // rows zeroed before CFAR
+    int nseg;
+    int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
+};
+
 constexpr int RSP_MAX_WIN = 16;
 
 struct MtdArgs {
@@ -92,20 +105,16 @@ struct MtdArgs {
     int rflag;
     uint32_t* hits;        // workgroup b owns hits[b*W*P, (b+1)*W*P) (its own cells: no overflow)
     uint32_t* hit_count;   // hit_count[b] = entries of workgroup b (b = blockIdx.y*gridDim.x + blockIdx.x)
+    // The previous chunk's range stage, run by extra workgroups of this launch (same stream,
+    // so that chunk's RDM and hit lists are complete): prev_nregions == 0 means none.
+    const float* prev_rdm;
+    uint8_t* prev_flag;
+    const uint32_t* prev_hits;
+    const uint32_t* prev_count;
+    int prev_nregions, prev_region;
+    CfarRArgs prev_cr;
 };
 
-// Range-dimension CFAR at the Doppler hits (executeCFAR.m:35-89).
-struct CfarRArgs {
-    int V, R;
-    int lo, hi;          // used rows
-    int rflag;
-    int ref, save, method;
-    float T;
-    float Tr;            // T / ref
-    int cz_lo, cz_hi;    // rows zeroed before CFAR
-    int nseg;
-    int seg_lo[RSP_MAX_SEG], seg_hi[RSP_MAX_SEG];
-};
 
 bool mtd_size_supported(int P, int beams = 1);
 bool pc_nfft_supported(int n);

@@ -742,6 +742,72 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums
     else doppler_rows_fixed<P, REF, false>(m, sums, cv, col_on, v0, o);
 }
 
+// One wave evaluates the hits of region rg: REF/SAVE > 0 compile-time windows (every load of
+// a hit's window issues at once); 0: the runtime ref/save of CfarRArgs.
+template <int REF, int SAVE>
+__device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, uint8_t* __restrict__ flag,
+                                                const uint32_t* __restrict__ hits,
+                                                const uint32_t* __restrict__ counts, int rg, int region,
+                                                const CfarRArgs& a, int lane) {
+    const uint32_t n = counts[rg];
+    const uint32_t* list = hits + (size_t)rg * region;
+    const int R = a.R, V = a.V;
+    const int ref = REF > 0 ? REF : a.ref, save = REF > 0 ? SAVE : a.save;
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint32_t idx = list[i];
+        const uint32_t row = idx / (uint32_t)R;        // cpi * V + v
+        const int r = (int)(idx - row * (uint32_t)R);
+        const int v = (int)(row % (uint32_t)V);
+        int slo, shi;
+        seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
+        if (shi <= slo) continue;
+        const bool zrow = v >= a.cz_lo && v < a.cz_hi;
+        const float* xr = rdm + (size_t)row * R;
+        auto X = [&](int c) { return (!zrow && c >= 0 && c < R) ? xr[c] : 0.f; };
+        int best = -1;
+        float bx = 0.f;
+#pragma unroll
+        for (int e = -1; e <= 1; ++e) {
+            const int q = r + e;
+            float sl = 0.f, sr = 0.f;
+            if constexpr (REF > 0) {
+#pragma unroll
+                for (int k = 0; k < REF; ++k) {
+                    sl += X(q - SAVE - REF + k);
+                    sr += X(q + SAVE + 1 + k);
+                }
+            } else {
+                for (int k = 0; k < ref; ++k) {
+                    sl += X(q - save - ref + k);
+                    sr += X(q + save + 1 + k);
+                }
+            }
+            const bool lok = q - save - ref >= slo, rok = q + save + ref < shi;
+            const float xq = X(q);
+            if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
+                best = q;
+                bx = xq;
+            }
+        }
+        if (best >= 0) flag[(size_t)row * R + best] = 1;
+    }
+}
+
+// The previous chunk's range stage inside an MTD launch: the extra row of workgroups
+// (blockIdx.y == gridDim.y - 1), one wave per hit region.
+__device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kBlock / 64;
+    const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
+    for (int rg = blockIdx.x * nw + w; rg < a.prev_nregions; rg += gridDim.x * nw) {
+        if (ref57)
+            cfar_hit_region<5, 7>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
+                                  lane);
+        else
+            cfar_hit_region<0, 0>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
+                                  lane);
+    }
+}
+
 // MTD: one workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the
 // tile, pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
 // samples load straight into registers with W-wide coalesced rows, the slow-time FFT runs
@@ -756,13 +822,18 @@ template <int P, int REF, int BEAMS>
 __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
+    const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
+    if (yoff && blockIdx.y == 0) {                  // dispatched first so it overlaps the tiles
+        prev_chunk_hits(a);
+        return;
+    }
     using C = MtdCfg<P>;
     constexpr int G = C::G, E = C::E, W = C::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_hits;
     if (threadIdx.x == 0) s_hits = 0u;   // published by the FFT's barriers
     const int c = threadIdx.x % W, g = threadIdx.x / W;
-    const size_t cpi = blockIdx.y;
+    const size_t cpi = blockIdx.y - yoff;
     const uint32_t R = (uint32_t)a.R_out;
     const int r = blockIdx.x * W + c;
     const bool rv = r < (int)R;
@@ -834,7 +905,7 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
     o.vo = rv ? (uint32_t)v0 * R + (uint32_t)r : kOob;
     o.R = R;
-    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t wg = (blockIdx.y - yoff) * gridDim.x + blockIdx.x;
     o.hits = a.hits ? a.hits + (size_t)wg * (W * P) : nullptr;
     o.lds_count = &s_hits;
     o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
@@ -863,13 +934,18 @@ template <int NF>
 __global__ __launch_bounds__(kBlock) void mtd_bluestein_kernel(const float2* __restrict__ pc,
                                                                float* __restrict__ rdm,
                                                                uint8_t* __restrict__ flagV, MtdArgs a) {
+    const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
+    if (yoff && blockIdx.y == 0) {                  // dispatched first so it overlaps the tiles
+        prev_chunk_hits(a);
+        return;
+    }
     using C = MtdCfg<NF>;
     constexpr int G = C::G, E = C::E, W = C::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_hits;
     if (threadIdx.x == 0) s_hits = 0u;
     const int c = threadIdx.x % W, g = threadIdx.x / W;
-    const size_t cpi = blockIdx.y;
+    const size_t cpi = blockIdx.y - yoff;
     const uint32_t R = (uint32_t)a.R_out;
     const int r = blockIdx.x * W + c;
     const bool rv = r < (int)R;
@@ -920,7 +996,7 @@ __global__ __launch_bounds__(kBlock) void mtd_bluestein_kernel(const float2* __r
     o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
     o.vo = (rv && v0 < P) ? (uint32_t)v0 * R + (uint32_t)r : kOob;
     o.R = R;
-    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t wg = (blockIdx.y - yoff) * gridDim.x + blockIdx.x;
     o.hits = a.hits ? a.hits + (size_t)wg * ((size_t)W * P) : nullptr;
     o.lds_count = &s_hits;
     o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
@@ -948,7 +1024,8 @@ static hipError_t launch_mtd_bluestein(const float2* pc, float* rdm, uint8_t* fl
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi), block(kBlock);
+    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
+        block(kBlock);
     hipLaunchKernelGGL((mtd_bluestein_kernel<NF>), grid, block, C::lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
@@ -970,7 +1047,8 @@ static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, in
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi), block(kBlock);
+    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
+        block(kBlock);
     hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, C::lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
@@ -1385,8 +1463,9 @@ __global__ __launch_bounds__(kBlock) void cfar_r16_kernel(const float* __restric
 // pick one cell; the writes are all 1.  Window sums are direct left-to-right adds.
 constexpr int kHitWaves = 4;   // regions per workgroup (one wave each)
 
-// REF/SAVE > 0: compile-time windows (every load of a hit's window issues at once);
-// 0: the runtime ref/save of CfarRArgs.
+
+
+
 template <int REF, int SAVE>
 __global__ __launch_bounds__(64 * kHitWaves) void cfar_hits_kernel(const float* __restrict__ rdm,
                                                                    uint8_t* __restrict__ flag,
@@ -1395,48 +1474,7 @@ __global__ __launch_bounds__(64 * kHitWaves) void cfar_hits_kernel(const float* 
                                                                    int region, CfarRArgs a) {
     const int rg = blockIdx.x * kHitWaves + (int)(threadIdx.x >> 6);
     if (rg >= nregions) return;
-    const uint32_t n = counts[rg];
-    const uint32_t* list = hits + (size_t)rg * region;
-    const int R = a.R, V = a.V;
-    const int ref = REF > 0 ? REF : a.ref, save = REF > 0 ? SAVE : a.save;
-    for (uint32_t i = threadIdx.x & 63; i < n; i += 64) {
-        const uint32_t idx = list[i];
-        const uint32_t row = idx / (uint32_t)R;        // cpi * V + v
-        const int r = (int)(idx - row * (uint32_t)R);
-        const int v = (int)(row % (uint32_t)V);
-        int slo, shi;
-        seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
-        if (shi <= slo) continue;
-        const bool zrow = v >= a.cz_lo && v < a.cz_hi;
-        const float* xr = rdm + (size_t)row * R;
-        auto X = [&](int c) { return (!zrow && c >= 0 && c < R) ? xr[c] : 0.f; };
-        int best = -1;
-        float bx = 0.f;
-#pragma unroll
-        for (int e = -1; e <= 1; ++e) {
-            const int q = r + e;
-            float sl = 0.f, sr = 0.f;
-            if constexpr (REF > 0) {
-#pragma unroll
-                for (int k = 0; k < REF; ++k) {
-                    sl += X(q - SAVE - REF + k);
-                    sr += X(q + SAVE + 1 + k);
-                }
-            } else {
-                for (int k = 0; k < ref; ++k) {
-                    sl += X(q - save - ref + k);
-                    sr += X(q + save + 1 + k);
-                }
-            }
-            const bool lok = q - save - ref >= slo, rok = q + save + ref < shi;
-            const float xq = X(q);
-            if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
-                best = q;
-                bx = xq;
-            }
-        }
-        if (best >= 0) flag[(size_t)row * R + best] = 1;
-    }
+    cfar_hit_region<REF, SAVE>(rdm, flag, hits, counts, rg, region, a, threadIdx.x & 63);
 }
 
 hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,

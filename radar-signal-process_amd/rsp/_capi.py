@@ -28,7 +28,8 @@ RSP_WIN_KAISER, RSP_WIN_HAMMING, RSP_WIN_RECT = 0, 1, 2
 EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_set_chunk",
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
-           "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev")
+           "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
+           "rsp_mtd_cfar_dev")
 RSP_NKERNELS = 4
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
 
@@ -104,6 +105,8 @@ def load_library(path=None):
                                                vp]
     lib.rsp_pc_mtd_cfar_diff_dev.restype = C.c_int
     lib.rsp_pc_mtd_cfar_diff_dev.argtypes = [vp, vp, i32, i64, C.POINTER(rsp_cfar_params), vp, vp, vp, vp, vp]
+    lib.rsp_mtd_cfar_dev.restype = C.c_int
+    lib.rsp_mtd_cfar_dev.argtypes = [vp, vp, i64, C.POINTER(rsp_cfar_params), vp, vp, vp, vp]
     lib.rsp_pc_dev.restype = C.c_int
     lib.rsp_pc_dev.argtypes = [vp, vp, i32, i64, vp, vp]
     lib.rsp_create_v2.restype = C.c_int

@@ -216,6 +216,28 @@ class Engine:
             self._stream_handle(stream))
         capi.check(rc, self.ctx)
 
+    def mtd_dev(self, pc, rdm=None, flag=None, flagV=None, cfar=None, stream=None):
+        """MTD + 0-v (+ CFAR) on pulse-compressed rows pc [batch, (beams,) P, R_out] complex64
+        (e.g. from pc_dev); outputs as run_dev."""
+        import torch
+        if not pc.is_cuda or not pc.is_contiguous() or pc.dtype != torch.complex64:
+            raise ValueError("pc must be a contiguous CUDA complex64 tensor")
+        batch = pc.shape[0]
+        want_in = (self.spec.P, self.spec.R_out) if self.spec.beams == 1 else (self.spec.beams, self.spec.P,
+                                                                              self.spec.R_out)
+        if tuple(pc.shape[1:]) != want_in:
+            raise ValueError("pc is %s, engine expects [batch, %s]" % (tuple(pc.shape), want_in))
+        want = (batch, self.spec.V, self.spec.R_out)
+        for t, dtp in ((rdm, torch.float32), (flag, torch.uint8), (flagV, torch.uint8)):
+            if t is not None and (tuple(t.shape) != want or t.dtype != dtp or not t.is_contiguous() or not t.is_cuda):
+                raise ValueError("output tensor must be contiguous CUDA %s of shape %s" % (dtp, want))
+        cp = cfar.to_c() if cfar is not None else None
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None   # noqa: E731
+        rc = self.lib.rsp_mtd_cfar_dev(self.ctx, C.c_void_p(pc.data_ptr()), batch,
+                                       C.byref(cp) if cp is not None else None, ptr(rdm), ptr(flag), ptr(flagV),
+                                       self._stream_handle(stream))
+        capi.check(rc, self.ctx)
+
     def pc_dev(self, echo, out, stream=None):
         """Pulse compression alone: out [batch, P, R_out] complex64."""
         import torch
