@@ -251,6 +251,11 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
                                        const PcMfArgs& a, int row, int t, float2* buf) {
     constexpr int E = N / G;
     constexpr bool kUniform = G % 64 == 0;
+    // Short rows (G <= 64, the segment that also carries the FIR): every global load of the
+    // row -- MF input and the whole spectrum slice -- is issued before the FIR, so one memory
+    // round trip overlaps the FIR instead of three in sequence.  Long rows keep the spectrum
+    // loads after the forward FFT (32 fewer live VGPRs across it).
+    constexpr bool kEarly = G <= 64;
     if constexpr (kUniform) row = __builtin_amdgcn_readfirstlane(row);
 #ifdef RSP_STAMPS
     const bool stamp_on = (N == 4096) && blockIdx.x < kStampBlocks;
@@ -260,16 +265,6 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     const bool valid = row < a.rows;
     const TIn* x = echo + (size_t)row * a.R;
     float2* y = out + (size_t)row * a.R_out;
-#ifndef RSP_AB_NOFIR
-    if (a.do_fir) {
-#else
-    if (false) {
-#endif
-        if (valid)
-            for (int z = 0; z < a.nzero; ++z)
-                for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) y[c] = make_float2(0.f, 0.f);
-        fir_row<TIn, G>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
-    }
     const int in_start = a.mf.in_start, in_len = a.mf.in_len;
     const int out_start = a.mf.out_start, out_len = a.mf.out_len;
     const float2* __restrict__ tw = a.mf.tw;
@@ -296,6 +291,21 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
         }
     }
+    float2 hs[kEarly ? E : 1];
+    if constexpr (kEarly) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+    }
+#ifndef RSP_AB_NOFIR
+    if (a.do_fir) {
+#else
+    if (false) {
+#endif
+        if (valid)
+            for (int z = 0; z < a.nzero; ++z)
+                for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) y[c] = make_float2(0.f, 0.f);
+        fir_row<TIn, G>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
+    }
 #ifdef RSP_STAMPS
     if (stamp_on) { float acc = 0.f; for (int m = 0; m < E; ++m) acc += u[m].x; asm volatile("" :: "v"(acc)); }
 #endif
@@ -303,16 +313,21 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     fft_reg_w<N, G, 1, E, 0, NW>(u, buf, t, w);
     RSP_STAMP(2);
 #ifndef RSP_AB_NOH
+    if constexpr (kEarly) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hs[m]);   // conj(X.*H), 1/N in H
+    } else {
 #ifndef RSP_HB
 #define RSP_HB 8
 #endif
 #pragma unroll
-    for (int m0 = 0; m0 < E; m0 += RSP_HB) {
-        float2 h[RSP_HB];   // batches of spectrum loads, then the multiply
+        for (int m0 = 0; m0 < E; m0 += RSP_HB) {
+            float2 h[RSP_HB];   // batches of spectrum loads, then the multiply
 #pragma unroll
-        for (int m = 0; m < RSP_HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * (m0 + m)) * 8u);
+            for (int m = 0; m < RSP_HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * (m0 + m)) * 8u);
 #pragma unroll
-        for (int m = 0; m < RSP_HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
+            for (int m = 0; m < RSP_HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
+        }
     }
 #endif
     RSP_STAMP(3);
@@ -400,6 +415,22 @@ __device__ __forceinline__ void mf_store(const float2 (&u)[N / G], float2* __res
     for (int m = 0; m < N / G; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
 }
 
+// The short-segment groups of a persistent PC workgroup: items first, +gridDim.x, ... < nitems.
+template <typename TIn, int N1, int N2>
+__device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, float2* __restrict__ out,
+                                               const PcMfArgs& a1, int n2, int nitems, int first, float2* lds) {
+#ifdef RSP_AB_NOSEG1
+    return;
+#endif
+    using PC = PairCfg<N1, N2>;
+    constexpr int G1 = PcCfg<N1>::G;
+    const int grp = threadIdx.x / G1, t1 = threadIdx.x % G1;
+    for (int item = first; item < nitems; item += (int)gridDim.x) {
+        __syncthreads();   // the previous item's last LDS reads are done
+        pc_row<TIn, N1, G1>(echo, out, a1, (item - n2) * PC::RPB1 + grp, t1, lds + grp * PcCfg<N1>::SLOT);
+    }
+}
+
 #ifndef RSP_PERSIST_WAVES
 #define RSP_PERSIST_WAVES 2
 #endif
@@ -409,11 +440,22 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
     using PC = PairCfg<N1, N2>;
     static_assert(PcCfg<N2>::G == PC::T, "one long-segment row per workgroup");
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    int item = blockIdx.x;
-    if (item < n2) {
+    // Items blockIdx.x, +gridDim.x, ...: the long rows (< n2) come first in that sequence, then
+    // the short groups.  Short groups are latency-bound (FIR + two small FFTs per row, little
+    // VALU), so odd workgroups run theirs first: the two workgroups sharing a CU are out of
+    // phase, and one's latency overlaps the other's FFT work.
+    const int first_short = (int)blockIdx.x < n2
+                                ? (int)blockIdx.x + ((n2 - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x) *
+                                                        (int)gridDim.x
+                                : (int)blockIdx.x;
+    const bool shorts_first = blockIdx.x & 1;
+    if (shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
+    if ((int)blockIdx.x < n2) {
+        int item = blockIdx.x;
         constexpr int G = PcCfg<N2>::G, E = N2 / G;
         constexpr int NW = tw_regs<N2, E>() > 0 ? tw_regs<N2, E>() : 1;
         const int t = threadIdx.x;
+        if (shorts_first) __syncthreads();   // the short items' last LDS reads are done
         float2 w[NW];
         tw_preload<N2, G, 1, E, 0, NW>(w, t, a2.mf.tw);
         float2 h[E];
@@ -445,15 +487,7 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
             item = next;
         }
     }
-#ifdef RSP_AB_NOSEG1
-    return;
-#endif
-    constexpr int G1 = PcCfg<N1>::G;
-    const int grp = threadIdx.x / G1, t1 = threadIdx.x % G1;
-    for (; item < nitems; item += (int)gridDim.x) {
-        __syncthreads();   // the previous item's last LDS reads are done
-        pc_row<TIn, N1, G1>(echo, out, a1, (item - n2) * PC::RPB1 + grp, t1, lds + grp * PcCfg<N1>::SLOT);
-    }
+    if (!shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
 }
 
 static int device_cus() {
