@@ -916,7 +916,7 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
         // fun_0v_pressing band, or the DMX zeroSetFlagMTD band wrapping through row 0
         if ((v >= a.z_lo && v < a.z_hi) || v + P < a.z_hi) x = 0.f;
         mg[m] = x;
-        buf_st_f(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
+        buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
     if (!a.cv.enabled) return;
     __syncthreads();  // the FFT exchange slots are free from here on
