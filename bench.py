@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--half", action="store_true", help="fp16 I/Q input")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
+    ap.add_argument("--fused", type=int, default=0, choices=[0, 1],
+                    help="1: one-launch fused chain where the shape has one; 0: chunked pipeline (library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--profile-every", type=int, default=7,
@@ -127,6 +129,7 @@ def main():
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
+    eng.set_fused(args.fused)
     B, P, R, win = args.batch, spec.P, spec.R_out, args.win
     units = B * win if win else B                   # CPIs (windows) per GPU per step
     # contiguous shard of the stream per rank (weak scaling): seed = 1000 + config id + first
@@ -171,7 +174,9 @@ def main():
     # timed steps with HIP events on the stream it is launched on (rsp_profile); read after
     # the timed region.  Sampling keeps the events' own cost out of the measured throughput.
     if not args.no_profile:
-        eng.profile(True, every=args.profile_every)
+        # a fused step is one or two launches: bracket each (the event pair is ~us of a ms step)
+        few = launches_per_step is not None and sum(launches_per_step.values()) <= 4
+        eng.profile(True, every=1 if few else args.profile_every)
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
@@ -182,6 +187,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    eng.chain_check()   # a fused launch whose bounded in-kernel wait expired invalidates the run
     elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, device=dev)
 
     kernels = None

@@ -225,14 +225,26 @@ int rsp_window_pc_mtd_cfar_dev(rsp_ctx* ctx, const void* d_frames, int32_t dtype
 int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, void* d_pc,
                void* stream);
 
+/* ---- execution strategy ------------------------------------------------------------------ */
+/* Fused chain (default off): where the context's shape has a fused kernel (one beam, no
+ * windows, P = 128 with the 1024 + 4096-point v2 segment pair), rsp_pc_mtd_cfar_dev and the
+ * host entry points run PC -> MTD -> CFAR of the whole call as ONE persistent launch, with
+ * the corner turn through a small ring of scratch CPIs instead of a chunk-sized scratch.
+ * enable = 0 selects the chunked two-kernel pipeline.  Results are bit-identical. */
+int rsp_set_fused(rsp_ctx* ctx, int32_t enable);
+/* Waits for the context's work and reports whether a fused launch gave up waiting for an
+ * item (a bounded in-kernel wait that expired): RSP_ERR_HIP with a message if so. */
+int rsp_chain_check(rsp_ctx* ctx);
+
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1
  * every N-th launch (sampling: each event pair costs the stream a few microseconds),
  * 0 stops.  Any call resets the counters.
- * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V. */
-#define RSP_NKERNELS 4
-enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3 };
+ * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V, RSP_K_CHAIN (the fused
+ * one-launch chain). */
+#define RSP_NKERNELS 5
+enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3, RSP_K_CHAIN = 4 };
 int rsp_profile(rsp_ctx* ctx, int32_t enable);
 /* Waits for the recorded events; ms[k] = summed device time, launches[k] = launch count. */
 int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches);

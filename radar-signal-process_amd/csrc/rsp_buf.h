@@ -57,4 +57,56 @@ __device__ __forceinline__ void buf_st_f_stream(float v, __amdgpu_buffer_rsrc_t 
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, kStreamAux);
 }
 
+// ---------------------------------------------------------------- in-launch hand-offs
+// The fused chain (chain_kernel) hands PC rows, RDM tiles and hit lists between workgroups
+// inside one launch.  Per-XCD L2s are not coherent, so every handed-off byte is stored
+// write-through (`sc1`, cache-policy aux 16) and every load of it is an `sc1` load (L1
+// bypassed, no acquire fence), with one agent-scope counter add per producing workgroup
+// after all its waves drained vmcnt (cdna_hip_programming.md Guideline 16, valid-form row 1).
+// Aux template argument: 0 = default policy, kSc1 = write-through / L1-bypass.
+#ifndef RSP_AB_HANDOFF_AUX
+#define RSP_AB_HANDOFF_AUX 16
+#endif
+constexpr int kSc1 = RSP_AB_HANDOFF_AUX;   // (ablation builds may set 0: plain, NOT coherent)
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+template <int AUX>
+__device__ __forceinline__ float2 buf_ld_f2a(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
+}
+template <int AUX>
+__device__ __forceinline__ float buf_ld_fa(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX));
+}
+template <int AUX>
+__device__ __forceinline__ void buf_st_f2a(float2 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    typedef int v2i __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), r, voff, soff, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void buf_st_fa(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, AUX);
+}
+// a single complex element through a plain pointer: plain, or an agent-scope relaxed
+// 8-byte atomic store (global_store_dwordx2 sc1)
+template <int AUX>
+__device__ __forceinline__ void st_c(float2* p, float2 v) {
+    if constexpr (AUX == 0) *p = v;
+    else __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_u32_sc1(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int AUX>
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
+    if constexpr (AUX == 0) return *p;
+    else return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int AUX>
+__device__ __forceinline__ float ld_f(const float* p) {
+    if constexpr (AUX == 0) return *p;
+    else return __builtin_bit_cast(float, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 }  // namespace rsp

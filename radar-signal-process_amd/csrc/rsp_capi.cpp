@@ -49,6 +49,8 @@ struct rsp_ctx {
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
+    bool fused = false;                 // one-launch chain where the shape has one (rsp_set_fused)
+    DevBuf chain_ctl;                   // fused chain: queue heads, stage counters, timeout word
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
     // diagnostics (rsp_profile): HIP event pairs around each kernel launch
     struct Ev {
@@ -201,7 +203,8 @@ int rsp_destroy(rsp_ctx* ctx) {
     hipSetDevice(ctx->device);
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
-                      &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t};
+                      &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
+                      &ctx->chain_ctl};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -730,6 +733,89 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
     return RSP_OK;
 }
 
+int rsp_set_fused(rsp_ctx* ctx, int32_t enable) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_fused: null ctx");
+    ctx->fused = enable != 0;
+    return RSP_OK;
+}
+
+int rsp_chain_check(rsp_ctx* ctx) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_chain_check: null ctx");
+    if (!ctx->chain_ctl.p) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    uint32_t tmo = 0;
+    HIP_TRY(ctx, hipMemcpy(&tmo, (uint32_t*)ctx->chain_ctl.p + (rsp::kChainCtlLines - 1) * rsp::kChainLine,
+                           sizeof(tmo), hipMemcpyDeviceToHost));
+    if (tmo) return fail(ctx, RSP_ERR_HIP, "fused chain: an in-kernel wait expired (results invalid)");
+    return RSP_OK;
+}
+
+// Whether the call can run as one fused launch (chain_kernel's shapes).
+static bool fused_ok(const rsp_ctx* ctx, int32_t dtype, int win, bool pc_input, const float* d_diff,
+                     const rsp::MtdArgs& m) {
+    if (!ctx->fused || pc_input || win > 0 || d_diff || ctx->beams != 1) return false;
+    if (dtype != RSP_C64 && dtype != RSP_C32F16) return false;
+    const int64_t P = ctx->p.P;
+    if (ctx->V != P || m.bnf != 0 || m.pin != P || !ctx->pc_v2 || ctx->pc_mf.size() != 2) return false;
+    if (!rsp::chain_supported((int)P, ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft, m.cv.ref)) return false;
+    const int W = rsp::chain_tile_width((int)P);
+    if (W <= 0 || m.shift % (int)(P / 16) != 0) return false;   // fftshift as a row rotation (G = P/16)
+    if (m.cv.enabled && m.cv.save + m.cv.ref + 2 > 32) return false;
+    return (uint64_t)P * ctx->p.R_out * 8 < 0x80000000ull;
+}
+
+// PC -> MTD -> CFAR of `ncpi` CPIs as one chain_kernel launch (rsp_internal.h ChainArgs).
+static int run_fused(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncpi, const rsp::MtdArgs& m,
+                     const rsp::CfarRArgs& cr, bool cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                     hipStream_t s) {
+    constexpr int NQ = rsp::kChainQueues, S = rsp::kChainSlots;
+    const int64_t P = ctx->p.P, Ro = ctx->p.R_out;
+    const size_t plane = (size_t)P * Ro;
+    if (ncpi > 0x7fffffff / 2) return fail(ctx, RSP_ERR_UNSUPPORTED, "fused chain: batch too large");
+    rsp::ChainArgs a{};
+    a.a1 = ctx->pc_mf[0];
+    a.a2 = ctx->pc_mf[1];
+    a.a1.rows = a.a2.rows = (int)P;
+    a.m = m;
+    a.m.rflag = cfar ? cr.rflag : 0;
+    a.cr = cr;
+    a.echo = d_echo;
+    a.ncpi = (int)ncpi;
+    const int W = rsp::chain_tile_width((int)P);
+    const int64_t nm = (Ro + W - 1) / W;
+    int rc = ensure(ctx, ctx->scratch_pc, (size_t)NQ * S * plane * sizeof(float2));
+    if (rc) return rc;
+    a.scratch = (float2*)ctx->scratch_pc.p;
+    a.rdm_ring = d_rdm == nullptr;
+    if (a.rdm_ring) {
+        rc = ensure(ctx, ctx->tmp_rdm, (size_t)NQ * S * plane * sizeof(float));
+        if (rc) return rc;
+        a.rdm = (float*)ctx->tmp_rdm.p;
+    } else {
+        a.rdm = d_rdm;
+    }
+    a.flag = cfar ? d_flag : nullptr;
+    a.flagV = cfar ? d_flagV : nullptr;
+    if (cfar && cr.rflag) {
+        rc = ensure(ctx, ctx->hit_list, (size_t)NQ * S * nm * W * P * sizeof(uint32_t));
+        if (rc) return rc;
+        rc = ensure(ctx, ctx->hit_ctr, (size_t)NQ * S * nm * sizeof(uint32_t));
+        if (rc) return rc;
+        a.hits = (uint32_t*)ctx->hit_list.p;
+        a.hit_count = (uint32_t*)ctx->hit_ctr.p;
+    }
+    const size_t ctl_bytes = (size_t)rsp::kChainCtlLines * rsp::kChainLine * sizeof(uint32_t);
+    rc = ensure(ctx, ctx->chain_ctl, ctl_bytes);
+    if (rc) return rc;
+    a.ctl = (uint32_t*)ctx->chain_ctl.p;
+    HIP_TRY(ctx, hipMemsetAsync(a.ctl, 0, ctl_bytes, s));
+    if (cfar && cr.rflag)   // background of the flag output; the range items write the 1s
+        HIP_TRY(ctx, hipMemsetAsync(d_flag, 0, (size_t)ncpi * plane, s));
+    HIP_TRY(ctx, timed(ctx, RSP_K_CHAIN, s, [&] { return rsp::launch_chain(dtype, a, s); }));
+    return RSP_OK;
+}
+
 // The chain over `units` on stream s.  win == 0: a unit is one CPI ([P][R] input rows).
 // win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
 // frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
@@ -747,6 +833,8 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
     } else {
         m.cv.enabled = 0;
     }
+    if (fused_ok(ctx, dtype, win, pc_input, d_diff, m))
+        return run_fused(ctx, d_echo, dtype, units, m, cr, cfar != nullptr, d_rdm, d_flag, d_flagV, s);
     const int64_t ocpi = win > 0 ? win : 1;               // output CPIs per unit
     m.nwin = win;
     for (int i = 0; i < win; ++i) m.win_start[i] = (int)mround((double)i * P / win);

@@ -199,7 +199,7 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
-template <typename TIn, int G>
+template <typename TIn, int G, int SA = 0>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t) {
     float2* s2 = reinterpret_cast<float2*>(stage);
@@ -232,7 +232,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
                 if (m < len) {
                     int n = m - g.fir_shift;
                     if (n < 0) n += len;
-                    y[g.out_start + n] = acc[i];
+                    st_c<SA>(y + g.out_start + n, acc[i]);
                 }
             }
         }
@@ -246,7 +246,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
 // SGPRs -- the zero padding beyond in_len, the out_len cut and invalid rows (num_records 0)
 // are the hardware range check, with no per-element branch.  G < 64 (N <= 512): rows share
 // a wave, so the accesses stay per-lane predicated.
-template <typename TIn, int N, int G>
+template <typename TIn, int N, int G, int SA = 0>
 __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
                                        const PcMfArgs& a, int row, int t, float2* buf) {
     constexpr int E = N / G;
@@ -303,8 +303,8 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #endif
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
-                for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) y[c] = make_float2(0.f, 0.f);
-        fir_row<TIn, G>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
+                for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) st_c<SA>(y + c, make_float2(0.f, 0.f));
+        fir_row<TIn, G, SA>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
     }
 #ifdef RSP_STAMPS
     if (stamp_on) { float acc = 0.f; for (int m = 0; m < E; ++m) acc += u[m].x; asm volatile("" :: "v"(acc)); }
@@ -339,12 +339,12 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         if (u[0].x == 12345.678f)
 #endif
 #pragma unroll
-        for (int m = 0; m < E; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+        for (int m = 0; m < E; ++m) buf_st_f2a<SA>(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
     } else if (valid) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int i = t + G * m;
-            if (i < out_len) y[out_start + i] = cconj(u[m]);
+            if (i < out_len) st_c<SA>(y + out_start + i, cconj(u[m]));
         }
     }
 #ifdef RSP_STAMPS
@@ -720,7 +720,7 @@ __device__ __forceinline__ void doppler_emit(const DopplerOut& o, bool hit, int 
                 uint32_t base = 0;
                 if (lane == leader) base = atomicAdd(o.lds_count, (uint32_t)__popcll(bal));
                 base = __shfl(base, leader);
-                if (hit) o.hits[base + __popcll(bal & ((1ull << lane) - 1))] = o.cell0 + so;
+                if (hit) st_u32_sc1(o.hits + base + __popcll(bal & ((1ull << lane) - 1)), o.cell0 + so);
             }
         }
     }
@@ -778,17 +778,17 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums
 
 // One wave evaluates the hits of region rg: REF/SAVE > 0 compile-time windows (every load of
 // a hit's window issues at once); 0: the runtime ref/save of CfarRArgs.
-template <int REF, int SAVE>
+template <int REF, int SAVE, int LA = 0>
 __device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, uint8_t* __restrict__ flag,
                                                 const uint32_t* __restrict__ hits,
                                                 const uint32_t* __restrict__ counts, int rg, int region,
                                                 const CfarRArgs& a, int lane) {
-    const uint32_t n = counts[rg];
+    const uint32_t n = ld_u32<LA>(counts + rg);
     const uint32_t* list = hits + (size_t)rg * region;
     const int R = a.R, V = a.V;
     const int ref = REF > 0 ? REF : a.ref, save = REF > 0 ? SAVE : a.save;
     for (uint32_t i = lane; i < n; i += 64) {
-        const uint32_t idx = list[i];
+        const uint32_t idx = ld_u32<LA>(list + i);
         const uint32_t row = idx / (uint32_t)R;        // cpi * V + v
         const int r = (int)(idx - row * (uint32_t)R);
         const int v = (int)(row % (uint32_t)V);
@@ -797,7 +797,7 @@ __device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, u
         if (shi <= slo) continue;
         const bool zrow = v >= a.cz_lo && v < a.cz_hi;
         const float* xr = rdm + (size_t)row * R;
-        auto X = [&](int c) { return (!zrow && c >= 0 && c < R) ? xr[c] : 0.f; };
+        auto X = [&](int c) { return (!zrow && c >= 0 && c < R) ? ld_f<LA>(xr + c) : 0.f; };
         int best = -1;
         float bx = 0.f;
 #pragma unroll
@@ -852,39 +852,43 @@ __device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a) {
 // P is the Doppler FFT length; a CPI supplies a.pin <= P pulses per beam (rows past pin are
 // the zero padding of fft(x, P, 1): out of the buffer's range, they load as 0).  BEAMS == 2:
 // the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
-template <int P, int REF, int BEAMS>
-__global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ pc,
-                                                     float* __restrict__ rdm,
-                                                     uint8_t* __restrict__ flagV, MtdArgs a) {
-    const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
-    if (yoff && blockIdx.y == 0) {                  // dispatched first so it overlaps the tiles
-        prev_chunk_hits(a);
-        return;
-    }
+// Pointers of one MTD work item: the CPI's planes and the tile's hit-list region.
+struct MtdTile {
+    const float2* pc;      // the CPI's first PC row (beam 0); beam b starts pin rows later
+    float* rdm;            // the CPI's RDM plane
+    float* diff;           // the CPI's DMX difference plane, or null
+    uint8_t* flagV;        // the CPI's flagV plane, or null
+    uint8_t* flag;         // the CPI's flag plane, or null (no CFAR)
+    uint32_t* hits;        // this tile's hit-list region (W*P entries), or null
+    uint32_t* hit_count;   // where the tile's hit count goes
+    uint32_t cell_base;    // hit-list number of the CPI's cell (0, 0)
+    int bx;                // tile index along range
+};
+
+// One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
+// the RDM stores (kSc1 when another workgroup of the same launch consumes them).
+template <int P, int REF, int BEAMS, int LA, int SA>
+__device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem,
+                                         uint32_t* s_hits) {
     using C = MtdCfg<P>;
     constexpr int G = C::G, E = C::E, W = C::W;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t s_hits;
-    if (threadIdx.x == 0) s_hits = 0u;   // published by the FFT's barriers
+    if (threadIdx.x == 0) *s_hits = 0u;   // published by the FFT's barriers
     const int c = threadIdx.x % W, g = threadIdx.x / W;
-    const size_t cpi = blockIdx.y - yoff;
     const uint32_t R = (uint32_t)a.R_out;
-    const int r = blockIdx.x * W + c;
+    const int r = T.bx * W + c;
     const bool rv = r < (int)R;
     const uint32_t plane = (uint32_t)P * R;                     // output plane (P Doppler rows)
     const uint32_t cell = (uint32_t)g * R + (uint32_t)r;        // element (g, r) of a plane
     const int pin = a.pin;
-    size_t row0 = cpi * (size_t)pin * BEAMS;                     // first PC row of this CPI
-    if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)pin + a.win_start[cpi % a.nwin];
     const uint32_t vo_in = rv ? cell * 8u : kOob;
     float2 u[E];
     float m0[BEAMS == 2 ? E : 1];     // |X_0| while beam 1 runs
 #pragma unroll
     for (int b = 0; b < BEAMS; ++b) {
-        const auto src = buf_rsrc(pc + (row0 + (size_t)b * pin) * R, (uint32_t)pin * R * 8u);
+        const auto src = buf_rsrc(T.pc + (size_t)b * pin * R, (uint32_t)pin * R * 8u);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float2 v = buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u);
+            const float2 v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
             const float w = a.win[g + G * m];
             u[m] = make_float2(v.x * w, v.y * w);
         }
@@ -897,9 +901,9 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
         }
     }
 
-    const auto dst = buf_rsrc(rdm + cpi * plane, plane * 4u);
-    const bool want_diff = BEAMS == 2 && a.diff != nullptr;
-    const auto dfr = buf_rsrc(want_diff ? a.diff + cpi * plane : nullptr, want_diff ? plane * 4u : 0u);
+    const auto dst = buf_rsrc(T.rdm, plane * 4u);
+    const bool want_diff = BEAMS == 2 && T.diff != nullptr;
+    const auto dfr = buf_rsrc(want_diff ? T.diff : nullptr, want_diff ? plane * 4u : 0u);
     const uint32_t vo_out = rv ? cell * 4u : kOob;
     const int srot = a.shift / G;
     float mg[E];
@@ -916,7 +920,8 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
         // fun_0v_pressing band, or the DMX zeroSetFlagMTD band wrapping through row 0
         if ((v >= a.z_lo && v < a.z_hi) || v + P < a.z_hi) x = 0.f;
         mg[m] = x;
-        buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
+        if constexpr (SA != 0) buf_st_fa<SA>(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
+        else buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
     if (!a.cv.enabled) return;
     __syncthreads();  // the FFT exchange slots are free from here on
@@ -932,17 +937,16 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     const int v0 = g * E;   // this thread's run of Doppler rows
     const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
     DopplerOut o;
-    o.want_fv = flagV != nullptr;
-    o.fused = a.flag != nullptr;
+    o.want_fv = T.flagV != nullptr;
+    o.fused = T.flag != nullptr;
     o.rflag = a.rflag != 0;
-    o.fv = buf_rsrc(o.want_fv ? flagV + cpi * plane : nullptr, o.want_fv ? plane : 0u);
-    o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
+    o.fv = buf_rsrc(o.want_fv ? T.flagV : nullptr, o.want_fv ? plane : 0u);
+    o.fl = buf_rsrc(o.fused ? T.flag : nullptr, o.fused ? plane : 0u);
     o.vo = rv ? (uint32_t)v0 * R + (uint32_t)r : kOob;
     o.R = R;
-    const uint32_t wg = (blockIdx.y - yoff) * gridDim.x + blockIdx.x;
-    o.hits = a.hits ? a.hits + (size_t)wg * (W * P) : nullptr;
-    o.lds_count = &s_hits;
-    o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
+    o.hits = T.hits;
+    o.lds_count = s_hits;
+    o.cell0 = T.cell_base + (uint32_t)v0 * R + (uint32_t)r;
     float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
     if constexpr (REF > 0) {
         doppler_cfar_fixed<P, REF>(mag, sums, a.cv, col_on, v0, o);
@@ -953,8 +957,49 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     }
     if (o.fused && o.rflag) {
         __syncthreads();
-        if (threadIdx.x == 0) a.hit_count[wg] = s_hits;
+        if (threadIdx.x == 0) st_u32_sc1(T.hit_count, *s_hits);
     }
+}
+
+// MTD: one workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the
+// tile, pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
+// samples load straight into registers with W-wide coalesced rows, the slow-time FFT runs
+// register-resident with LDS exchanges, and |X| leaves in coalesced RDM rows.  The fftshift
+// offset is 0 or P/2, a multiple of G, so bin g + G*m lands in row g + G*((m + shift/G) mod E):
+// a wave-uniform rotation, and every row offset is an SGPR operand of the buffer access.
+// REF > 0: Doppler CFAR specialised on the reference window; REF == 0: runtime window.
+// P is the Doppler FFT length; a CPI supplies a.pin <= P pulses per beam (rows past pin are
+// the zero padding of fft(x, P, 1): out of the buffer's range, they load as 0).  BEAMS == 2:
+// the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
+template <int P, int REF, int BEAMS>
+__global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ pc,
+                                                     float* __restrict__ rdm,
+                                                     uint8_t* __restrict__ flagV, MtdArgs a) {
+    const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
+    if (yoff && blockIdx.y == 0) {                  // dispatched first so it overlaps the tiles
+        prev_chunk_hits(a);
+        return;
+    }
+    using C = MtdCfg<P>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_hits;
+    const size_t cpi = blockIdx.y - yoff;
+    const size_t R = (size_t)a.R_out;
+    const size_t plane = (size_t)P * R;
+    size_t row0 = cpi * (size_t)a.pin * BEAMS;                   // first PC row of this CPI
+    if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)a.pin + a.win_start[cpi % a.nwin];
+    const uint32_t wg = (blockIdx.y - yoff) * gridDim.x + blockIdx.x;
+    MtdTile T;
+    T.pc = pc + row0 * R;
+    T.rdm = rdm + cpi * plane;
+    T.diff = (BEAMS == 2 && a.diff) ? a.diff + cpi * plane : nullptr;
+    T.flagV = flagV ? flagV + cpi * plane : nullptr;
+    T.flag = a.flag ? a.flag + cpi * plane : nullptr;
+    T.hits = a.hits ? a.hits + (size_t)wg * (C::W * P) : nullptr;
+    T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
+    T.cell_base = (uint32_t)(cpi * plane);
+    T.bx = blockIdx.x;
+    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
@@ -1636,6 +1681,230 @@ hipError_t launch_transpose_f32(const float* in, float* out, int64_t batch, int 
 hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, int A, int B,
                                hipStream_t s) {
     return launch_transpose_t(in, out, batch, A, B, s);
+}
+
+// ================================================================== fused chain (one launch)
+// PC -> MTD (+Doppler CFAR) -> range CFAR of a whole call in one persistent launch; the work
+// queues and their ordering are described with ChainArgs (rsp_internal.h).  Hand-offs
+// between the stages cross workgroups (and XCDs) inside the launch, so they follow the
+// write-through protocol of rsp_buf.h: the PC scratch, the RDM and the hit lists are stored
+// `sc1`, every storing wave drains vmcnt before its workgroup's one counter add, and every
+// load of handed-off bytes is an `sc1` load issued after thread 0 saw the counter.  The
+// corner turn's scratch is a ring of kChainSlots CPIs per queue (96 MiB at 128 x 4096), so it
+// is re-read from the Infinity Cache a few CPIs after it was written, instead of from HBM.
+__device__ __forceinline__ uint32_t* chain_head(uint32_t* ctl, int h) { return ctl + h * kChainLine; }
+__device__ __forceinline__ uint32_t* chain_ctr(uint32_t* ctl, int h, int slot) {
+    return ctl + (kChainQueues + h * kChainSlots + slot) * kChainLine;
+}
+__device__ __forceinline__ uint32_t chain_claim(uint32_t* ctl, int h) {
+    return __hip_atomic_fetch_add((gu32*)chain_head(ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0: wait until *p >= target (relaxed agent-scope polls with s_sleep between).  A
+// wait that lasts 0.5 s sets the timeout word, and once it is set no wait blocks: the launch
+// then completes with wrong data (reported by rsp_chain_check) instead of hanging the GPU.
+__device__ __forceinline__ void chain_wait(uint32_t* p, uint32_t target, uint32_t* tmo) {
+#ifdef RSP_AB_NOWAIT
+    return;
+#endif
+    if (__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s of the 100 MHz clock
+            __hip_atomic_fetch_or((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
+// Every wave drains its stores, then thread 0 publishes the workgroup's item.
+__device__ __forceinline__ void chain_signal(uint32_t* p) {
+#ifndef RSP_AB_NODRAIN
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int N1, int N2, int P>
+struct ChainCfg {
+    using PC = PairCfg<N1, N2>;
+    using MC = MtdCfg<P>;
+    static constexpr size_t main = PC::lds > MC::lds ? PC::lds : MC::lds;
+    static constexpr size_t lds = ((main + 15) & ~(size_t)15) + 16;   // + control words
+};
+
+template <typename TIn, int N1, int N2, int P, int REF>
+__device__ __forceinline__ void chain_item(const ChainArgs& a, int h, uint32_t q, unsigned char* smem,
+                                           uint32_t* s_hits, uint32_t* tmo) {
+    constexpr int S = kChainSlots, D = kChainLag;
+    using PC = PairCfg<N1, N2>;
+    using MC = MtdCfg<P>;
+    const int tid = threadIdx.x;
+    const int npc = a.nl + a.nsh;
+    const int ips = npc + a.nm + a.nh;
+    const int seg = (int)(q / (uint32_t)ips), k = (int)(q % (uint32_t)ips);
+    int j, kind, idx;
+    if (k < npc) { j = seg; kind = 0; idx = k; }
+    else if (k < npc + a.nm) { j = seg - D; kind = 1; idx = k - npc; }
+    else { j = seg - D - 1; kind = 2; idx = k - npc - a.nm; }
+    const int c = h + kChainQueues * j;
+    if (j < 0 || c >= a.ncpi) return;
+    const int slot = j % S;
+    const uint32_t gen = (uint32_t)(j / S);
+    uint32_t* ctr = chain_ctr(a.ctl, h, slot);
+    const size_t R = (size_t)a.a2.R, Ro = (size_t)a.a2.R_out;
+    const size_t plane = (size_t)P * Ro;
+    const size_t ring = (size_t)(h * S + slot);
+    float2* pcs = a.scratch + ring * P * Ro;
+    float* rdm = a.rdm_ring ? a.rdm + ring * plane : a.rdm + (size_t)c * plane;
+    constexpr uint32_t region = (uint32_t)(MC::W * P);
+    if (kind == 0) {   // one PC item: a long-segment row, or PC::RPB1 short-segment rows
+        if (tid == 0 && gen > 0) chain_wait(ctr + 1, gen * (uint32_t)a.nm, tmo);   // slot free
+        __syncthreads();
+        const TIn* ein = (const TIn*)a.echo + (size_t)c * P * R;
+        if (idx < a.nl) {
+            pc_row<TIn, N2, kBlock, kSc1>(ein, pcs, a.a2, idx, tid, reinterpret_cast<float2*>(smem));
+        } else {
+            constexpr int G1 = PcCfg<N1>::G;
+            const int grp = tid / G1;
+            pc_row<TIn, N1, G1, kSc1>(ein, pcs, a.a1, (idx - a.nl) * PC::RPB1 + grp, tid % G1,
+                                      reinterpret_cast<float2*>(smem) + grp * PcCfg<N1>::SLOT);
+        }
+        chain_signal(ctr + 0);
+    } else if (kind == 1) {   // one MTD tile (+ Doppler CFAR, hit list)
+        if (tid == 0) {
+            chain_wait(ctr + 0, (gen + 1) * (uint32_t)npc, tmo);                     // CPI's PC
+            if (a.nh > 0 && gen > 0) chain_wait(ctr + 2, gen * (uint32_t)a.nh, tmo);  // hit slot free
+        }
+        __syncthreads();
+        MtdTile T;
+        T.pc = pcs;
+        T.rdm = rdm;
+        T.diff = nullptr;
+        T.flagV = a.flagV ? a.flagV + (size_t)c * plane : nullptr;
+        T.flag = a.flag ? a.flag + (size_t)c * plane : nullptr;
+        T.hits = a.nh > 0 ? a.hits + (ring * a.nm + idx) * region : nullptr;
+        T.hit_count = a.nh > 0 ? a.hit_count + ring * a.nm + idx : nullptr;
+        T.cell_base = 0;
+        T.bx = idx;
+        mtd_tile<P, REF, 1, kSc1, kSc1>(T, a.m, smem, s_hits);
+        chain_signal(ctr + 1);
+    } else {   // range CFAR at the Doppler hits of a run of the CPI's tiles (one wave per tile)
+        if (tid == 0) chain_wait(ctr + 1, (gen + 1) * (uint32_t)a.nm, tmo);
+        __syncthreads();
+        const int lane = tid & 63, w = tid >> 6;
+        const uint32_t* hl = a.hits + ring * a.nm * region;
+        const uint32_t* hc = a.hit_count + ring * a.nm;
+        uint8_t* fl = a.flag + (size_t)c * plane;
+        const int per = (a.nm + a.nh - 1) / a.nh;
+        const int r0 = idx * per, r1 = r0 + per < a.nm ? r0 + per : a.nm;
+        const bool ref57 = a.cr.ref == 5 && a.cr.save == 7;
+        for (int rg = r0 + w; rg < r1; rg += kBlock / 64) {
+            if (ref57) cfar_hit_region<5, 7, kSc1>(rdm, fl, hl, hc, rg, region, a.cr, lane);
+            else cfar_hit_region<0, 0, kSc1>(rdm, fl, hl, hc, rg, region, a.cr, lane);
+        }
+        chain_signal(ctr + 2);
+    }
+}
+
+template <typename TIn, int N1, int N2, int P, int REF>
+__global__ __launch_bounds__(kBlock, RSP_PERSIST_WAVES) void chain_kernel(ChainArgs a) {
+    using CC = ChainCfg<N1, N2, P>;
+    static_assert(CC::PC::T == kBlock && PcCfg<N2>::G == kBlock, "one long-segment row per workgroup");
+    static_assert(CC::MC::W * CC::MC::G == kBlock, "MTD tile shape");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* sw = reinterpret_cast<uint32_t*>(smem + ((CC::main + 15) & ~(size_t)15));   // [0] item, [1] hits
+    const int tid = threadIdx.x;
+    const int ips = a.nl + a.nsh + a.nm + a.nh;
+    const int extra = a.nh > 0 ? kChainLag + 1 : kChainLag;
+    uint32_t* tmo = a.ctl + (kChainCtlLines - 1) * kChainLine;
+    int h = (int)(blockIdx.x % kChainQueues);   // home queue; placement changes speed only
+    auto total = [&](int qh) -> uint32_t {
+        const int J = a.ncpi > qh ? (a.ncpi - qh + kChainQueues - 1) / kChainQueues : 0;
+        return J > 0 ? (uint32_t)(J + extra) * (uint32_t)ips : 0u;
+    };
+    if (tid == 0) sw[0] = chain_claim(a.ctl, h);
+    __syncthreads();
+    // the item number is wave-uniform: readfirstlane keeps everything derived from it in SGPRs
+    // (buffer resources built from a VGPR value would need waterfall loops)
+    uint32_t q = __builtin_amdgcn_readfirstlane(sw[0]);
+    int tried = 1;
+    for (;;) {
+        __syncthreads();   // every thread has read sw[0]
+        if (q >= total(h)) {   // queue drained: steal from the next one
+            if (tried == kChainQueues) break;
+            ++tried;
+            h = (h + 1) % kChainQueues;
+            if (tid == 0) sw[0] = chain_claim(a.ctl, h);
+            __syncthreads();
+            q = __builtin_amdgcn_readfirstlane(sw[0]);
+            continue;
+        }
+        uint32_t nxt = 0;
+        if (tid == 0) nxt = chain_claim(a.ctl, h);   // claim ahead: its latency overlaps the item
+        // Re-read the arguments inside every item: an opaque copy of the kernarg pointer stops
+        // the compiler from hoisting every field any item type uses into SGPRs for the whole
+        // loop (hundreds of SGPR spills otherwise).
+        // (the kernel's only argument sits at offset 0 of the kernarg segment)
+        typedef const __attribute__((address_space(4))) ChainArgs ChainArgsK;
+        const ChainArgsK* ap = (const ChainArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        chain_item<TIn, N1, N2, P, REF>(*(const ChainArgs*)ap, h, q, smem, sw + 1, tmo);
+        __syncthreads();
+        if (tid == 0) sw[0] = nxt;
+        __syncthreads();
+        q = __builtin_amdgcn_readfirstlane(sw[0]);
+    }
+}
+
+template <typename TIn, int N1, int N2, int P, int REF>
+static hipError_t launch_chain_t(ChainArgs& a, hipStream_t s) {
+    using CC = ChainCfg<N1, N2, P>;
+    static int resident = 0;
+    if (!resident) {
+        hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<TIn, N1, N2, P, REF>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CC::lds);
+        if (e != hipSuccess) return e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)chain_kernel<TIn, N1, N2, P, REF>,
+                                                         kBlock, CC::lds);
+        if (e != hipSuccess) return e;
+        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
+    }
+    a.nl = P;
+    a.nsh = (P + CC::PC::RPB1 - 1) / CC::PC::RPB1;
+    a.nm = (a.a2.R_out + CC::MC::W - 1) / CC::MC::W;
+    a.nh = (a.flag && a.cr.rflag) ? (a.nm + 31) / 32 : 0;
+    const int64_t items = (int64_t)a.ncpi * (a.nl + a.nsh + a.nm + a.nh);
+    a.grid = items < resident ? (int)items : resident;
+    if (a.grid < 1) return hipSuccess;
+    hipLaunchKernelGGL((chain_kernel<TIn, N1, N2, P, REF>), dim3((unsigned)a.grid), dim3(kBlock), CC::lds, s, a);
+    return hipGetLastError();
+}
+
+bool chain_supported(int P, int n1, int n2, int ref) {
+    (void)ref;
+    return P == 128 && n1 == 1024 && n2 == 4096;
+}
+
+int chain_tile_width(int P) { return P == 128 ? MtdCfg<128>::W : 0; }
+
+template <typename TIn>
+static hipError_t launch_chain_d(ChainArgs& a, hipStream_t s) {
+    const bool ref5 = a.m.cv.enabled && a.m.cv.ref == 5;
+    if (a.m.P == 128 && a.a1.mf.nfft == 1024 && a.a2.mf.nfft == 4096)
+        return ref5 ? launch_chain_t<TIn, 1024, 4096, 128, 5>(a, s) : launch_chain_t<TIn, 1024, 4096, 128, 0>(a, s);
+    return hipErrorNotSupported;
+}
+
+hipError_t launch_chain(int dtype, ChainArgs& a, hipStream_t s) {
+    if (a.ncpi <= 0) return hipSuccess;
+    if (dtype == RSP_C64) return launch_chain_d<float2>(a, s);
+    if (dtype == RSP_C32F16) return launch_chain_d<__half2>(a, s);
+    return hipErrorInvalidValue;
 }
 
 }  // namespace rsp

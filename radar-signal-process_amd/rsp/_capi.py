@@ -29,9 +29,9 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
-           "rsp_mtd_cfar_dev")
-RSP_NKERNELS = 4
-KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
+           "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check")
+RSP_NKERNELS = 5
+KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "chain_kernel")
 
 
 class RspError(RuntimeError):
@@ -114,6 +114,10 @@ def load_library(path=None):
                                   C.POINTER(C.c_double)]
     lib.rsp_set_streams.restype = C.c_int
     lib.rsp_set_streams.argtypes = [vp, i32]
+    lib.rsp_set_fused.restype = C.c_int
+    lib.rsp_set_fused.argtypes = [vp, i32]
+    lib.rsp_chain_check.restype = C.c_int
+    lib.rsp_chain_check.argtypes = [vp]
     lib.rsp_profile.restype = C.c_int
     lib.rsp_profile.argtypes = [vp, i32]
     lib.rsp_profile_read.restype = C.c_int

@@ -59,6 +59,14 @@ class Engine:
     def set_chunk(self, cpis):
         capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)
 
+    def set_fused(self, enable):
+        """One-launch fused chain where the shape has one (1); 0 = chunked pipeline (default)."""
+        capi.check(self.lib.rsp_set_fused(self.ctx, int(enable)), self.ctx)
+
+    def chain_check(self):
+        """Raise if a fused launch of this context gave up waiting for an item."""
+        capi.check(self.lib.rsp_chain_check(self.ctx), self.ctx)
+
     @property
     def shape(self):
         """(Doppler rows, range bins) of one RDM."""
