@@ -779,6 +779,7 @@ static int run_fused(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t nc
     a.a1.rows = a.a2.rows = (int)P;
     a.m = m;
     a.m.rflag = cfar ? cr.rflag : 0;
+    a.m.flag_zero = 0;   // in-launch hand-off: the flag plane is memset before the launch
     a.cr = cr;
     a.echo = d_echo;
     a.ncpi = (int)ncpi;
@@ -868,8 +869,10 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
         rc = ensure(ctx, ctx->tmp_rdm, (size_t)2 * ns * cells * sizeof(float));
         if (rc) return rc;
     }
-    if (cfar && cr.rflag)   // background of the whole flag output; the range stage writes the 1s
-        HIP_TRY(ctx, hipMemsetAsync(d_flag, 0, (size_t)units * ocpi * plane, s));
+    // the MTD kernels write the flag plane's zero background with the Doppler stage (every cell
+    // of a CPI belongs to one MTD thread), and the range stage, stream-ordered after that
+    // chunk's MTD launch, writes the 1s: no separate fill pass
+    m.flag_zero = 1;
     // Chunk k runs on lane k % ns (lane 0 = the caller's stream), each lane with its own
     // scratch slot, so PC of one chunk overlaps MTD / CFAR of the previous one.  The lanes
     // fork from and join back into the caller's stream.

@@ -103,6 +103,7 @@ struct MtdArgs {
     // then sets the re-localised range detections.  flagV is written only when requested.
     uint8_t* flag;
     int rflag;
+    int flag_zero;         // rflag: the MTD kernel writes the flag plane's zeros (else the host memsets it)
     uint32_t* hits;        // workgroup b owns hits[b*W*P, (b+1)*W*P) (its own cells: no overflow)
     uint32_t* hit_count;   // hit_count[b] = entries of workgroup b (b = blockIdx.y*gridDim.x + blockIdx.x)
     // The previous chunk's range stage, run by extra workgroups of this launch (same stream,

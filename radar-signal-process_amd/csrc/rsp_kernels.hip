@@ -205,9 +205,30 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
     float2* s2 = reinterpret_cast<float2*>(stage);
     const int kp = g.ntaps4 - 1;
     const int len = g.out_len;
-    for (int i = t; i < kp + len + 4; i += G) {
-        const int j = i - kp;
-        s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+    const int nst = kp + len + 4;
+    if constexpr (G % 64 == 0) {
+        // The row is wave-uniform: stage through a range-checked buffer resource, 8 loads per
+        // thread issued together (zeros before the segment and past in_len come from the range
+        // check), so the staging costs one memory round trip instead of one per element step.
+        constexpr uint32_t ES = sizeof(TIn);
+        const auto xr = buf_rsrc(x + g.in_start, valid ? (uint32_t)g.in_len * ES : 0u);
+        constexpr int B = 8;
+        for (int i0 = t; i0 < nst; i0 += B * G) {
+            float2 v[B];
+#pragma unroll
+            for (int q = 0; q < B; ++q) {
+                const int j = i0 + q * G - kp;
+                v[q] = buf_ld_c((const TIn*)nullptr, xr, j >= 0 ? (uint32_t)j * ES : kOob, 0u);
+            }
+#pragma unroll
+            for (int q = 0; q < B; ++q)
+                if (i0 + q * G < nst) s2[i0 + q * G] = v[q];
+        }
+    } else {
+        for (int i = t; i < nst; i += G) {
+            const int j = i - kp;
+            s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+        }
     }
     __syncthreads();
     const float2* __restrict__ taps = g.taps2_dev;
@@ -403,14 +424,22 @@ __device__ __forceinline__ void mf_load(float2 (&u)[N / G], const TIn* __restric
     constexpr uint32_t ES = sizeof(TIn);
     const auto xr = buf_rsrc(echo + (size_t)row * a.R + a.mf.in_start, valid ? (uint32_t)a.mf.in_len * ES : 0u);
 #pragma unroll
-    for (int m = 0; m < N / G; ++m)
+    for (int m = 0; m < N / G; ++m) {
+#ifdef RSP_AB_NOLOAD
+        u[m] = make_float2((float)(t + G * m + row), a.mf.scale);
+#else
         u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
+#endif
+    }
 }
 
 template <int N, int G>
 __device__ __forceinline__ void mf_store(const float2 (&u)[N / G], float2* __restrict__ out, const PcMfArgs& a,
                                          int row, int t) {
     const auto yr = buf_rsrc(out + (size_t)row * a.R_out + a.mf.out_start, (uint32_t)a.mf.out_len * 8u);
+#ifdef RSP_AB_NOSTORE
+    if (u[0].x == 12345.678f)
+#endif
 #pragma unroll
     for (int m = 0; m < N / G; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
 }
@@ -433,6 +462,9 @@ __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, flo
 
 #ifndef RSP_PERSIST_WAVES
 #define RSP_PERSIST_WAVES 2
+#endif
+#ifndef RSP_PC_DEPTH
+#define RSP_PC_DEPTH 1   // long rows in flight ahead of the one being transformed (1 or 2)
 #endif
 template <typename TIn, int N1, int N2>
 __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_persist_kernel(
@@ -464,6 +496,42 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
         for (int m = 0; m < E; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
         float2 u[E];
         mf_load<TIn, N2, G>(u, echo, a2, item, true, t);
+#if RSP_PC_DEPTH == 2
+        // Two rows in flight: three register buffers rotate (row item, item+grid loaded,
+        // item+2*grid loading), unrolled three times so no buffer is ever copied -- a copy
+        // would make the compiler wait for the youngest loads at the end of every row.  Each
+        // row's loads are issued after the forward FFT of the row two steps earlier, so they
+        // have ~1.5 rows of work to land; before a row's stores only the OLDER prefetch is
+        // waited for (vmcnt is in order), the younger one stays in flight.
+        float2 b1[E], b2[E];
+        {
+            const int nx1 = item + (int)gridDim.x;
+            mf_load<TIn, N2, G>(b1, echo, a2, nx1 < n2 ? nx1 : item, nx1 < n2, t);
+        }
+#pragma unroll
+        for (int m = 0; m < E; ++m) asm volatile("" ::"v"(u[m]), "v"(h[m]));
+        const int gs = (int)gridDim.x;
+        auto step = [&](float2 (&cur)[E], float2 (&pf)[E], const float2 (&older)[E]) {
+            fft_reg_w<N2, G, 1, E, 0, NW>(cur, lds, t, w);
+            const int nx2 = item + 2 * gs;
+            mf_load<TIn, N2, G>(pf, echo, a2, nx2 < n2 ? nx2 : item, nx2 < n2, t);
+#pragma unroll
+            for (int m = 0; m < E; ++m) cur[m] = cmul_conj(cur[m], h[m]);   // conj(X.*H), 1/N in H
+            fft_reg_w<N2, G, 1, E, 0, NW>(cur, lds, t, w);
+#pragma unroll
+            for (int m = 0; m < E; ++m) asm volatile("" ::"v"(older[m]));
+            mf_store<N2, G>(cur, out, a2, item, t);
+            item += gs;
+        };
+        for (;;) {
+            if (item >= n2) break;
+            step(u, b2, b1);
+            if (item >= n2) break;
+            step(b1, u, b2);
+            if (item >= n2) break;
+            step(b2, b1, u);
+        }
+#else
         // settle the entry loads here, so the loop header carries no pending load (a merged
         // wait state would put a vmcnt(0) -- a store drain -- at the top of every iteration)
 #pragma unroll
@@ -486,6 +554,7 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
             for (int m = 0; m < E; ++m) u[m] = nx[m];
             item = next;
         }
+#endif
     }
     if (!shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
 }
@@ -686,14 +755,16 @@ struct MtdCfg {
     static constexpr size_t lds_fft = (size_t)W * SLOT * sizeof(float2);
     static constexpr size_t lds_cfar = (size_t)W * (MS + SMS) * sizeof(float);
     static constexpr size_t lds = lds_fft > lds_cfar ? lds_fft : lds_cfar;
+    // REF > 0: the window sums stay in registers; LDS holds only a padded magnitude column
+    // (SPAD pad cells on each side, odd stride), inside the FFT exchange area
+    static constexpr int MS2 = P + 2 * SPAD + 1;
+    static constexpr size_t lds_cfar_reg = (size_t)W * MS2 * sizeof(float);
+    static constexpr size_t lds_reg = lds_fft > lds_cfar_reg ? lds_fft : lds_cfar_reg;
+    template <int REF>
+    static constexpr size_t lds_for() { return REF > 0 ? lds_reg : lds; }
     static_assert(G * E == P && (G & (G - 1)) == 0 && G <= kBlock, "MTD tiling");
 };
 
-// Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
-// guard `save` and the row band stay runtime).  The thread's run of E rows plus REF-1
-// look-ahead rows is read from LDS once; its E window sums are direct left-to-right adds
-// (the order mean() uses) and go to a padded sums column, so the left/right window lookups
-// of every row are unclamped LDS reads with immediate offsets.
 // Per-row outputs of the Doppler CFAR at cell (v, r) of launch CPI `cpi`: flagV (if requested),
 // the flag plane's background (flagV when the range stage is off, else 0) and, for a hit
 // with the range stage on, an entry in the hit list (one atomic per wave and row).
@@ -705,6 +776,7 @@ struct DopplerOut {
     uint32_t* lds_count;             // workgroup hit counter (LDS)
     uint32_t cell0;                  // linear index of (v0, r) within the launch
     bool want_fv, fused, rflag;
+    bool zero_bg;                    // rflag: write the flag plane's zero background here
 };
 
 __device__ __forceinline__ void doppler_emit(const DopplerOut& o, bool hit, int i) {
@@ -712,7 +784,8 @@ __device__ __forceinline__ void doppler_emit(const DopplerOut& o, bool hit, int 
     if (o.want_fv) buf_st_u8(hit ? 1 : 0, o.fv, o.vo, so);
     if (o.fused) {
         if (!o.rflag) buf_st_u8(hit ? 1 : 0, o.fl, o.vo, so);   // flag = flagV (executeCFAR.m:91)
-        else {   // flag plane pre-zeroed by the host; the range stage sets the detections
+        else {   // zero background (here, or pre-zeroed by the host); the range stage sets the detections
+            if (o.zero_bg) buf_st_u8(0, o.fl, o.vo, so);
             const uint64_t bal = __ballot(hit);
             if (bal) {   // rare: hits are sparse
                 const int lane = __lane_id();
@@ -731,49 +804,50 @@ __device__ __forceinline__ void doppler_flags(const float* mag, const float* sum
     for (int v = v0; v < v1; ++v) doppler_emit(o, doppler_test(mag, sums, cv, col_on, v) != 0, v - v0);
 }
 
-template <int P, int REF, bool GO>
-__device__ __forceinline__ void doppler_rows_fixed(const float* m, const float* sums, const CfarVArgs& cv,
-                                                   bool col_on, int v0, const DopplerOut& o) {
-    constexpr int E = MtdCfg<P>::E;
+// Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
+// guard `save`, the method and the row band stay runtime).  A thread owns a run of E rows of
+// one range column: it reads its rows, their left windows and their right windows from the
+// padded magnitude column once (three bases, immediate offsets) and forms all 2E window sums
+// in registers -- no sums array, no second barrier, and the LDS footprint stays inside the
+// FFT exchange area (one more resident workgroup per CU than a sums column allows).
+template <int P, int REF>
+__device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarVArgs& cv, bool col_on, int v0,
+                                                   const DopplerOut& o) {
+    // mag: this column's magnitudes, mag[v] for v in [-SPAD, P + SPAD) (pad cells unused:
+    // every row in [lo, hi) has at least one window inside the column, the other is selected
+    // away).  The left window of row v0+i starts at v0+i-save-REF, the right one at
+    // v0+i+save+1; each sum is the direct left-to-right add of its REF cells (mean()'s order).
+    constexpr int E = MtdCfg<P>::E, NL = E + REF - 1;
+    const float* bl = mag + v0 - cv.save - REF;
+    const float* br = mag + v0 + cv.save + 1;
+    const float* bm = mag + v0;
+    float L[NL], Rw[NL], m[E];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        L[i] = bl[i];
+        Rw[i] = br[i];
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) m[i] = bm[i];
     const int kl = cv.lo + cv.save + REF - v0;     // row v0+i has a left window iff i >= kl
     const int kr = cv.hi - cv.save - 1 - REF - v0; // ... and a right window iff i <= kr
     const int b0 = cv.lo - v0, b1 = cv.hi - v0;    // tested rows: b0 <= i < b1
-    const float* sl_p = sums + v0 - cv.save - REF;
-    const float* sr_p = sums + v0 + cv.save + 1;
+    const bool go = cv.method == 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-        const float sl = sl_p[i], sr = sr_p[i];    // pad / other rows when unused: selected away
+        float sl = L[i], sr = Rw[i];
+#pragma unroll
+        for (int q = 1; q < REF; ++q) {
+            sl += L[i + q];
+            sr += Rw[i + q];
+        }
         const bool lok = i >= kl, rok = i <= kr;
         const float x = lok ? sl : sr, y = rok ? sr : sl;   // one-sided fallback (:30-39)
         // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
-        const float th = (GO ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
+        const float th = (go ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
         const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
         doppler_emit(o, hit, i);
     }
-}
-
-// Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
-// guard `save`, the method and the row band stay runtime).  The thread's run of E rows plus
-// REF-1 look-ahead rows is read from LDS once; its E window sums are direct left-to-right
-// adds (the order mean() uses) and go to a padded sums column, so every row's left/right
-// window lookups are unclamped LDS reads with immediate offsets.
-template <int P, int REF>
-__device__ __forceinline__ void doppler_cfar_fixed(const float* mag, float* sums, const CfarVArgs& cv,
-                                                   bool col_on, int v0, const DopplerOut& o) {
-    constexpr int E = MtdCfg<P>::E;
-    float m[E + REF - 1];
-#pragma unroll
-    for (int i = 0; i < E + REF - 1; ++i) m[i] = mag[v0 + i];   // rows >= P: unused garbage
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-        float acc = m[i];
-#pragma unroll
-        for (int k = 1; k < REF; ++k) acc += m[i + k];
-        sums[v0 + i] = acc;
-    }
-    __syncthreads();
-    if (cv.method == 0) doppler_rows_fixed<P, REF, true>(m, sums, cv, col_on, v0, o);
-    else doppler_rows_fixed<P, REF, false>(m, sums, cv, col_on, v0, o);
 }
 
 // One wave evaluates the hits of region rg: REF/SAVE > 0 compile-time windows (every load of
@@ -925,7 +999,8 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     }
     if (!a.cv.enabled) return;
     __syncthreads();  // the FFT exchange slots are free from here on
-    float* mag = reinterpret_cast<float*>(smem) + c * C::MS;
+    float* mag = REF > 0 ? reinterpret_cast<float*>(smem) + c * C::MS2 + C::SPAD
+                         : reinterpret_cast<float*>(smem) + c * C::MS;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         int mm = m + srot;
@@ -940,6 +1015,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     o.want_fv = T.flagV != nullptr;
     o.fused = T.flag != nullptr;
     o.rflag = a.rflag != 0;
+    o.zero_bg = a.flag_zero != 0;
     o.fv = buf_rsrc(o.want_fv ? T.flagV : nullptr, o.want_fv ? plane : 0u);
     o.fl = buf_rsrc(o.fused ? T.flag : nullptr, o.fused ? plane : 0u);
     o.vo = rv ? (uint32_t)v0 * R + (uint32_t)r : kOob;
@@ -947,10 +1023,10 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     o.hits = T.hits;
     o.lds_count = s_hits;
     o.cell0 = T.cell_base + (uint32_t)v0 * R + (uint32_t)r;
-    float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
     if constexpr (REF > 0) {
-        doppler_cfar_fixed<P, REF>(mag, sums, a.cv, col_on, v0, o);
+        doppler_cfar_fixed<P, REF>(mag, a.cv, col_on, v0, o);
     } else {
+        float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
         doppler_sums(mag, sums, P, a.cv.ref, v0, v0 + E);
         __syncthreads();
         doppler_flags(mag, sums, a.cv, col_on, v0, v0 + E, o);
@@ -1071,6 +1147,7 @@ __global__ __launch_bounds__(kBlock) void mtd_bluestein_kernel(const float2* __r
     o.want_fv = flagV != nullptr;
     o.fused = a.flag != nullptr;
     o.rflag = a.rflag != 0;
+    o.zero_bg = a.flag_zero != 0;
     o.fv = buf_rsrc(o.want_fv ? flagV + cpi * plane : nullptr, o.want_fv ? plane : 0u);
     o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
     o.vo = (rv && v0 < P) ? (uint32_t)v0 * R + (uint32_t)r : kOob;
@@ -1119,16 +1196,17 @@ template <int P, int REF, int BEAMS>
 static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                 const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P>;
+    constexpr size_t lds = C::template lds_for<REF>();
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P, REF, BEAMS>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::lds);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
         block(kBlock);
-    hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, C::lds, s, pc, rdm, flagV, a);
+    hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
 
