@@ -449,7 +449,20 @@ __device__ __forceinline__ void tw_preload(float2 (&w)[NW], int t, const float2*
 }
 
 // fft_reg with the twiddles of every pass already in registers (w from tw_preload)
-template <int N, int G, int Ns, int E, int WO, int NW>
+// Exchange synchronisation: the workgroup barrier, or (WS: the transform belongs to one wave)
+// a wave-scope fence -- a wave's LDS operations are performed in issue order.
+template <bool WS>
+__device__ __forceinline__ void xsync() {
+    if constexpr (WS) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
+template <int N, int G, int Ns, int E, int WO, int NW, bool WS = false>
 __device__ __forceinline__ void fft_reg_w(float2 (&u)[E], float2* buf, int t, const float2 (&w)[NW]) {
     if constexpr (Ns < N) {
         constexpr int R = pick_radix_e(N / Ns, E);
@@ -477,7 +490,7 @@ __device__ __forceinline__ void fft_reg_w(float2 (&u)[E], float2* buf, int t, co
             for (int r = 0; r < R; ++r) u[i + r * PER] = v[r];
         }
         if constexpr (Ns * R < N) {
-            __syncthreads();  // WAR: earlier readers of buf are done
+            xsync<WS>();  // WAR: earlier readers of buf are done
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int j = t + i * G;
@@ -485,10 +498,90 @@ __device__ __forceinline__ void fft_reg_w(float2 (&u)[E], float2* buf, int t, co
 #pragma unroll
                 for (int r = 0; r < R; ++r) buf[slot<Ns, R>(base, r)] = u[i + r * PER];
             }
-            __syncthreads();  // RAW
+            xsync<WS>();  // RAW
         }
-        fft_reg_w<N, G, Ns * R, E, WO + (Ns > 1 ? PER * L : 0), NW>(u, buf, t, w);
+        fft_reg_w<N, G, Ns * R, E, WO + (Ns > 1 ? PER * L : 0), NW, WS>(u, buf, t, w);
     }
+}
+
+// ---------------------------------------------------------------- 64-point register DFT
+// W64^k, k < 48, fp32-rounded from fp64 (the products b*c of dft64 stay below 46)
+__device__ constexpr float kW64[48][2] = {
+    {1.000000000e+00f, 0.000000000e+00f},
+    {9.951847196e-01f, -9.801714122e-02f},
+    {9.807852507e-01f, -1.950903237e-01f},
+    {9.569403529e-01f, -2.902846634e-01f},
+    {9.238795042e-01f, -3.826834261e-01f},
+    {8.819212914e-01f, -4.713967443e-01f},
+    {8.314695954e-01f, -5.555702448e-01f},
+    {7.730104327e-01f, -6.343932748e-01f},
+    {7.071067691e-01f, -7.071067691e-01f},
+    {6.343932748e-01f, -7.730104327e-01f},
+    {5.555702448e-01f, -8.314695954e-01f},
+    {4.713967443e-01f, -8.819212914e-01f},
+    {3.826834261e-01f, -9.238795042e-01f},
+    {2.902846634e-01f, -9.569403529e-01f},
+    {1.950903237e-01f, -9.807852507e-01f},
+    {9.801714122e-02f, -9.951847196e-01f},
+    {6.123234263e-17f, -1.000000000e+00f},
+    {-9.801714122e-02f, -9.951847196e-01f},
+    {-1.950903237e-01f, -9.807852507e-01f},
+    {-2.902846634e-01f, -9.569403529e-01f},
+    {-3.826834261e-01f, -9.238795042e-01f},
+    {-4.713967443e-01f, -8.819212914e-01f},
+    {-5.555702448e-01f, -8.314695954e-01f},
+    {-6.343932748e-01f, -7.730104327e-01f},
+    {-7.071067691e-01f, -7.071067691e-01f},
+    {-7.730104327e-01f, -6.343932748e-01f},
+    {-8.314695954e-01f, -5.555702448e-01f},
+    {-8.819212914e-01f, -4.713967443e-01f},
+    {-9.238795042e-01f, -3.826834261e-01f},
+    {-9.569403529e-01f, -2.902846634e-01f},
+    {-9.807852507e-01f, -1.950903237e-01f},
+    {-9.951847196e-01f, -9.801714122e-02f},
+    {-1.000000000e+00f, -1.224646853e-16f},
+    {-9.951847196e-01f, 9.801714122e-02f},
+    {-9.807852507e-01f, 1.950903237e-01f},
+    {-9.569403529e-01f, 2.902846634e-01f},
+    {-9.238795042e-01f, 3.826834261e-01f},
+    {-8.819212914e-01f, 4.713967443e-01f},
+    {-8.314695954e-01f, 5.555702448e-01f},
+    {-7.730104327e-01f, 6.343932748e-01f},
+    {-7.071067691e-01f, 7.071067691e-01f},
+    {-6.343932748e-01f, 7.730104327e-01f},
+    {-5.555702448e-01f, 8.314695954e-01f},
+    {-4.713967443e-01f, 8.819212914e-01f},
+    {-3.826834261e-01f, 9.238795042e-01f},
+    {-2.902846634e-01f, 9.569403529e-01f},
+    {-1.950903237e-01f, 9.807852507e-01f},
+    {-9.801714122e-02f, 9.951847196e-01f}
+
+};
+
+// In-place natural-order DFT of 64 registers: n = 16a + b, k = c + 4d,
+//   X[c + 4d] = sum_b W16^{bd} [ W64^{bc} sum_a x[16a + b] W4^{ac} ]
+// -- 16 DFT4 (stride 16), 45 constant twiddles, 4 DFT16 (contiguous), a register rename.
+__device__ __forceinline__ void dft64(float2 (&v)[64]) {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) dft4(v[b], v[16 + b], v[32 + b], v[48 + b]);
+#pragma unroll
+    for (int c = 1; c < 4; ++c) {
+#pragma unroll
+        for (int b = 1; b < 16; ++b) {
+            const int e = b * c;
+            if (e == 16) v[b + 16 * c] = cmul_mj(v[b + 16 * c]);
+            else v[b + 16 * c] = cmul(v[b + 16 * c], make_float2(kW64[e][0], kW64[e][1]));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dft16(&v[16 * c]);
+    float2 x[64];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 16; ++d) x[c + 4 * d] = v[16 * c + d];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = x[k];
 }
 
 }  // namespace rsp

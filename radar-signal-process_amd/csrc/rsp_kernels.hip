@@ -199,7 +199,7 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
-template <typename TIn, int G, int SA = 0>
+template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t) {
     float2* s2 = reinterpret_cast<float2*>(stage);
@@ -230,7 +230,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
         }
     }
-    __syncthreads();
+    xsync<WS>();
     const float2* __restrict__ taps = g.taps2_dev;
     for (int m0 = 4 * t; m0 < len; m0 += 4 * G) {
         float2 acc[4] = {};
@@ -258,7 +258,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             }
         }
     }
-    __syncthreads();
+    xsync<WS>();
 }
 
 // One row's matched-filter segment (and optionally its FIR segment) by G threads.
@@ -267,7 +267,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
 // SGPRs -- the zero padding beyond in_len, the out_len cut and invalid rows (num_records 0)
 // are the hardware range check, with no per-element branch.  G < 64 (N <= 512): rows share
 // a wave, so the accesses stay per-lane predicated.
-template <typename TIn, int N, int G, int SA = 0>
+template <typename TIn, int N, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
                                        const PcMfArgs& a, int row, int t, float2* buf) {
     constexpr int E = N / G;
@@ -325,13 +325,13 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
                 for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) st_c<SA>(y + c, make_float2(0.f, 0.f));
-        fir_row<TIn, G, SA>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
+        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
     }
 #ifdef RSP_STAMPS
     if (stamp_on) { float acc = 0.f; for (int m = 0; m < E; ++m) acc += u[m].x; asm volatile("" :: "v"(acc)); }
 #endif
     RSP_STAMP(1);
-    fft_reg_w<N, G, 1, E, 0, NW>(u, buf, t, w);
+    fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
     RSP_STAMP(2);
 #ifndef RSP_AB_NOH
     if constexpr (kEarly) {
@@ -352,7 +352,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     }
 #endif
     RSP_STAMP(3);
-    fft_reg_w<N, G, 1, E, 0, NW>(u, buf, t, w);
+    fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
     RSP_STAMP(4);
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
@@ -460,8 +460,11 @@ __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, flo
     }
 }
 
+#ifndef RSP_PC_LEAN
+#define RSP_PC_LEAN 0
+#endif
 #ifndef RSP_PERSIST_WAVES
-#define RSP_PERSIST_WAVES 2
+#define RSP_PERSIST_WAVES (RSP_PC_LEAN ? 4 : 2)
 #endif
 #ifndef RSP_PC_DEPTH
 #define RSP_PC_DEPTH 1   // long rows in flight ahead of the one being transformed (1 or 2)
@@ -488,6 +491,44 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
         constexpr int NW = tw_regs<N2, E>() > 0 ? tw_regs<N2, E>() : 1;
         const int t = threadIdx.x;
         if (shorts_first) __syncthreads();   // the short items' last LDS reads are done
+#if RSP_PC_LEAN
+        // Lean register plan (for 4 resident workgroups per CU): twiddles and the spectrum
+        // slice are re-loaded per row instead of living in registers for the whole launch.
+        // Load issue order keeps every wait off the younger loads (vmcnt is in order):
+        //   [fwd FFT: twiddles tf] -> issue ti -> multiply (H) -> issue next row -> IFFT (ti)
+        //   -> wait next row -> issue tf, H for the next row -> stores
+        // so the peak live set is u + 2 of {twiddles, H, next row} (~90 VGPRs + temporaries).
+        const auto hr = buf_rsrc(a2.mf.H, (uint32_t)N2 * 8u);
+        float2 u[E], tf[NW], hh[E];
+        mf_load<TIn, N2, G>(u, echo, a2, item, true, t);
+#pragma unroll
+        for (int m = 0; m < E; ++m) asm volatile("" ::"v"(u[m]));
+        tw_preload<N2, G, 1, E, 0, NW>(tf, t, a2.mf.tw);
+#pragma unroll
+        for (int m = 0; m < E; ++m) hh[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+        while (item < n2) {
+            const int next = item + (int)gridDim.x;
+            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, tf);
+            float2 ti[NW];
+            tw_preload<N2, G, 1, E, 0, NW>(ti, t, a2.mf.tw);
+#pragma unroll
+            for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hh[m]);   // conj(X.*H), 1/N in H
+            float2 nx[E];
+            mf_load<TIn, N2, G>(nx, echo, a2, next < n2 ? next : item, next < n2, t);
+            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, ti);
+#pragma unroll
+            for (int m = 0; m < E; ++m) asm volatile("" ::"v"(nx[m]));
+            if (next < n2) {
+                tw_preload<N2, G, 1, E, 0, NW>(tf, t, a2.mf.tw);
+#pragma unroll
+                for (int m = 0; m < E; ++m) hh[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+            }
+            mf_store<N2, G>(u, out, a2, item, t);
+#pragma unroll
+            for (int m = 0; m < E; ++m) u[m] = nx[m];
+            item = next;
+        }
+#else
         float2 w[NW];
         tw_preload<N2, G, 1, E, 0, NW>(w, t, a2.mf.tw);
         float2 h[E];
@@ -555,8 +596,128 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
             item = next;
         }
 #endif
+#endif   // RSP_PC_LEAN
     }
     if (!shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
+}
+
+#ifndef RSP_PC_WAVE
+#define RSP_PC_WAVE 0   // the 1024 + 4096 pair as one wave per row (pc_wave_kernel): measured slower
+#endif
+// ---------------------------------------------------------------- one wave per 4096-point row
+// The 4096-point matched filter as a 64 x 64 four-step transform owned by ONE wave: lane t
+// holds x[t + 64m] (m < 64, 128 VGPRs), and
+//   pass 1: DFT64 over m in registers -> Y[t][k1]; twiddle W4096^{t k1};
+//   corner turn through the wave's LDS slot (lane t writes row t, lane k reads column k);
+//   pass 2: DFT64 over n1 in registers -> X[k1 + 64 k2] in register k2 (natural order: the
+//   input pattern of the inverse transform, of the spectrum loads and of coalesced stores).
+// No workgroup barrier anywhere (a wave's LDS operations are performed in issue order) and one
+// LDS exchange per transform instead of two.  The corner turn moves the real and the
+// imaginary halves in turn through a 64 x 65-float slot (16.6 KB per wave), so two workgroups
+// of four waves fit a CU.  Short-segment rows (FIR + N1-point MF) run one row per wave too.
+constexpr int kWaveStride = 65;                  // floats per slot row (odd: b32 row writes and column reads conflict-free)
+constexpr int kWaveSlot = 64 * kWaveStride;      // floats per wave
+
+// twiddle bases of lane t: B[i] = W4096^{t i}, A[j] = W4096^{8 t j} (i, j < 8), from the table
+// (offsets recomputed per call: an opaque lane copy keeps them from being hoisted out of the
+// row loop, where 16 loop-invariant addresses would be spilled)
+__device__ __forceinline__ void tw4096_bases(float2 (&A)[8], float2 (&B)[8], const float2* __restrict__ tw, int lane) {
+    const auto tr = buf_rsrc(tw, 4096u * 8u);
+    uint32_t l8 = (uint32_t)lane * 8u;
+    asm volatile("" : "+v"(l8));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        B[i] = buf_ld_f2(tr, l8 * (uint32_t)i, 0u);
+        A[i] = buf_ld_f2(tr, l8 * (uint32_t)(8 * i), 0u);
+    }
+}
+
+// Y[t][m] *= W4096^{t m} = A[m / 8] * B[m % 8]
+__device__ __forceinline__ void tw4096(float2 (&v)[64], const float2 (&A)[8], const float2 (&B)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i == 0 && j == 0) continue;
+            const float2 w = (j == 0) ? B[i] : (i == 0 ? A[j] : cmul(A[j], B[i]));
+            v[8 * j + i] = cmul(v[8 * j + i], w);
+        }
+    }
+}
+
+// corner turn: lane t's v[m] = Y[t][m]  ->  lane k's v[n] = Y[n][k]; real halves, then imaginary
+__device__ __forceinline__ void turn64(float2 (&v)[64], float* slot, int lane) {
+    float* row = slot + lane * kWaveStride;
+#pragma unroll
+    for (int m = 0; m < 64; ++m) row[m] = v[m].x;
+    xsync<true>();
+#pragma unroll
+    for (int n = 0; n < 64; ++n) v[n].x = slot[n * kWaveStride + lane];
+    xsync<true>();
+#pragma unroll
+    for (int m = 0; m < 64; ++m) row[m] = v[m].y;
+    xsync<true>();
+#pragma unroll
+    for (int n = 0; n < 64; ++n) v[n].y = slot[n * kWaveStride + lane];
+    xsync<true>();
+}
+
+__device__ __forceinline__ void fft4096_wave(float2 (&v)[64], float* slot, int lane, const float2* __restrict__ tw) {
+    float2 A[8], B[8];
+    tw4096_bases(A, B, tw, lane);   // table loads (L1/L2 hits) land during the first DFT64
+    dft64(v);
+    tw4096(v, A, B);
+    turn64(v, slot, lane);
+    dft64(v);
+}
+
+// One long-segment row (4096-point matched filter) by one wave.
+template <typename TIn>
+__device__ __forceinline__ void pc_long_wave(const TIn* __restrict__ echo, float2* __restrict__ out,
+                                             const PcMfArgs& a, int row, int lane, float* slot) {
+    constexpr uint32_t ES = sizeof(TIn);
+    row = __builtin_amdgcn_readfirstlane(row);
+    const auto xr = buf_rsrc(echo + (size_t)row * a.R + a.mf.in_start, (uint32_t)a.mf.in_len * ES);
+    float2 v[64];
+#pragma unroll
+    for (int m = 0; m < 64; ++m) v[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)lane * ES, (uint32_t)(64 * m) * ES);
+    fft4096_wave(v, slot, lane, a.mf.tw);
+    const auto hr = buf_rsrc(a.mf.H, 4096u * 8u);
+#pragma unroll
+    for (int m0 = 0; m0 < 64; m0 += 16) {
+        float2 h[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) h[m] = buf_ld_f2(hr, (uint32_t)lane * 8u, (uint32_t)(64 * (m0 + m)) * 8u);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m0 + m] = cmul_conj(v[m0 + m], h[m]);   // conj(X.*H), 1/N in H
+    }
+    fft4096_wave(v, slot, lane, a.mf.tw);
+    const auto yr = buf_rsrc(out + (size_t)row * a.R_out + a.mf.out_start, (uint32_t)a.mf.out_len * 8u);
+#pragma unroll
+    for (int m = 0; m < 64; ++m) buf_st_f2(cconj(v[m]), yr, (uint32_t)lane * 8u, (uint32_t)(64 * m) * 8u);
+}
+
+// Items gw, gw + nw, ... of the launch's 2*rows: [0, rows) long rows, [rows, 2 rows) short rows.
+template <typename TIn, int N1>
+#ifndef RSP_PC_WAVE_WPS
+#define RSP_PC_WAVE_WPS 2   // waves per SIMD the register budget is sized for (1: 512 incl. AGPRs)
+#endif
+__global__ __launch_bounds__(256, RSP_PC_WAVE_WPS) void pc_wave_kernel(const TIn* __restrict__ echo, float2* __restrict__ out,
+                                                         PcMfArgs a1, PcMfArgs a2, int rows) {
+    static_assert(PcCfg<N1>::G == 64 && (size_t)padded_len(N1) * 2 <= (size_t)kWaveSlot, "short row = one wave");
+    extern __shared__ __attribute__((aligned(16))) float lds_f[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* slot = lds_f + wv * kWaveSlot;
+    const int gw = (int)blockIdx.x * 4 + wv, nw = (int)gridDim.x * 4;
+    for (int item = gw; item < 2 * rows; item += nw) {
+        // an opaque lane copy per item: lane-derived addresses are recomputed inside the item
+        // instead of being hoisted out of the loop (and spilled)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        if (item < rows) pc_long_wave<TIn>(echo, out, a2, item, ln, slot);
+        else pc_row<TIn, N1, 64, 0, true>(echo, out, a1, item - rows, ln, reinterpret_cast<float2*>(slot));
+    }
 }
 
 static int device_cus() {
@@ -592,6 +753,30 @@ static hipError_t launch_pc_persist(const TIn* echo, float2* out, const PcMfArgs
     return hipGetLastError();
 }
 
+#if RSP_PC_WAVE
+template <typename TIn, int N1>
+static hipError_t launch_pc_wave(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs& a2,
+                                 hipStream_t s) {
+    constexpr size_t lds = (size_t)4 * kWaveSlot * sizeof(float);
+    static int resident = 0;
+    if (!resident) {
+        hipError_t e = hipFuncSetAttribute((const void*)pc_wave_kernel<TIn, N1>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_wave_kernel<TIn, N1>, 256, lds);
+        if (e != hipSuccess) return e;
+        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
+    }
+    const int rows = a1.rows;
+    const int want = (2 * rows + 3) / 4;
+    const int grid = want < resident ? want : resident;
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL((pc_wave_kernel<TIn, N1>), dim3((unsigned)grid), dim3(256), lds, s, echo, out, a1, a2, rows);
+    return hipGetLastError();
+}
+#endif
+
 bool pc_mf_supported(int nfft, int fir_stage_len) {
     switch (nfft) {
         case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: case 8192:
@@ -625,10 +810,16 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
 #ifndef RSP_PC_PERSIST
 #define RSP_PC_PERSIST 1
 #endif
+#if RSP_PC_WAVE
+#define RSP_PC_WAVE_LAUNCH(n1, n2) if (n2 == 4096) return launch_pc_wave<TIn, n1>(echo, out, a1, *a2, s);
+#else
+#define RSP_PC_WAVE_LAUNCH(n1, n2)
+#endif
 #define RSP_PAIR(n1, n2) \
     if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s)
 #define RSP_PAIR_PERSIST(n1, n2)                                                              \
     if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) {                                        \
+        RSP_PC_WAVE_LAUNCH(n1, n2)                                                            \
         if (RSP_PC_PERSIST) return launch_pc_persist<TIn, n1, n2>(echo, out, a1, *a2, s);     \
         return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s);                             \
     }
@@ -1965,7 +2156,7 @@ static hipError_t launch_chain_t(ChainArgs& a, hipStream_t s) {
 
 bool chain_supported(int P, int n1, int n2, int ref) {
     (void)ref;
-    return P == 128 && n1 == 1024 && n2 == 4096;
+    return PairCfg<1024, 4096>::T == kBlock && P == 128 && n1 == 1024 && n2 == 4096;
 }
 
 int chain_tile_width(int P) { return P == 128 ? MtdCfg<128>::W : 0; }
@@ -1973,8 +2164,11 @@ int chain_tile_width(int P) { return P == 128 ? MtdCfg<128>::W : 0; }
 template <typename TIn>
 static hipError_t launch_chain_d(ChainArgs& a, hipStream_t s) {
     const bool ref5 = a.m.cv.enabled && a.m.cv.ref == 5;
-    if (a.m.P == 128 && a.a1.mf.nfft == 1024 && a.a2.mf.nfft == 4096)
-        return ref5 ? launch_chain_t<TIn, 1024, 4096, 128, 5>(a, s) : launch_chain_t<TIn, 1024, 4096, 128, 0>(a, s);
+    if constexpr (PairCfg<1024, 4096>::T == kBlock) {   // (a PC build with other row widths has no chain)
+        if (a.m.P == 128 && a.a1.mf.nfft == 1024 && a.a2.mf.nfft == 4096)
+            return ref5 ? launch_chain_t<TIn, 1024, 4096, 128, 5>(a, s) : launch_chain_t<TIn, 1024, 4096, 128, 0>(a, s);
+    }
+    (void)ref5;
     return hipErrorNotSupported;
 }
 
