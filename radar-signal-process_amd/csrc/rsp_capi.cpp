@@ -859,7 +859,7 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
         if (cells > 0xffffffffull) return fail(ctx, RSP_ERR_UNSUPPORTED, "chunk too large for 32-bit hit indices");
         // two slots per lane: chunk k's list is read by the next MTD launch on its lane while
         // that launch fills the other slot
-        rsp::mtd_regions((int)V, (int)Ro, (int)(cu * ocpi), &nreg, &reg);
+        rsp::mtd_regions((int)V, (int)Ro, (int)(cu * ocpi), &nreg, &reg, (int)NB);
         rc = ensure(ctx, ctx->hit_list, (size_t)2 * ns * nreg * reg * sizeof(uint32_t));
         if (rc) return rc;
         rc = ensure(ctx, ctx->hit_ctr, (size_t)2 * ns * nreg * sizeof(uint32_t));
@@ -935,7 +935,7 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
             Pending& pv = pend[lane];
-            rsp::mtd_regions((int)V, (int)Ro, (int)ncpi, &pv.nreg, &pv.reg);   // this chunk's workgroups
+            rsp::mtd_regions((int)V, (int)Ro, (int)ncpi, &pv.nreg, &pv.reg, (int)NB);   // this chunk's workgroups
             pv.rdm = rdm;
             pv.flag = m.flag;
             pv.hits = m.hits;

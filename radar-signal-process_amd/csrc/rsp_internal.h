@@ -176,7 +176,7 @@ hipError_t launch_cfar_v(const float* rdm, uint8_t* flagV, int ncpi, int V, int 
 hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
                             int nregions, int region, const CfarRArgs& a, hipStream_t s);
 // MTD workgroups per launch and cells per workgroup (hit-list regions)
-void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region);
+void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region, int beams = 1);
 // Bluestein convolution length for a P without a radix plan (0: unsupported)
 int mtd_bluestein_nf(int P);
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,

@@ -934,9 +934,15 @@ __device__ __forceinline__ void doppler_flags(const float* mag, const float* sum
 // pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
 // samples load straight into registers with W-wide coalesced rows, the slow-time FFT
 // runs register-resident with LDS exchanges, and |X| leaves in coalesced RDM rows.
-template <int P>
+template <int P, int BEAMS = 1>
 struct MtdCfg {
-    static constexpr int E = (P % 3 == 0) ? 24 : 16;   // elements per thread
+    // elements per thread: 32 from P = 512 on (one beam), so a tile keeps >= 16 range bins
+    // (>= 128-B row segments) as P grows; 16 below and for the two-beam pair (whose second
+    // beam's magnitudes already take E registers); 24 for the 3*2^k lengths
+#ifndef RSP_MTD_WIDE
+#define RSP_MTD_WIDE 1
+#endif
+    static constexpr int E = (P % 3 == 0) ? 24 : ((RSP_MTD_WIDE && BEAMS == 1 && P >= 512) ? 32 : 16);
     static constexpr int G = P / E;                    // threads per range bin
     static constexpr int W = kBlock / G;               // range bins per workgroup
     static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
@@ -1001,14 +1007,14 @@ __device__ __forceinline__ void doppler_flags(const float* mag, const float* sum
 // padded magnitude column once (three bases, immediate offsets) and forms all 2E window sums
 // in registers -- no sums array, no second barrier, and the LDS footprint stays inside the
 // FFT exchange area (one more resident workgroup per CU than a sums column allows).
-template <int P, int REF>
+template <int P, int REF, int BEAMS>
 __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarVArgs& cv, bool col_on, int v0,
                                                    const DopplerOut& o) {
     // mag: this column's magnitudes, mag[v] for v in [-SPAD, P + SPAD) (pad cells unused:
     // every row in [lo, hi) has at least one window inside the column, the other is selected
     // away).  The left window of row v0+i starts at v0+i-save-REF, the right one at
     // v0+i+save+1; each sum is the direct left-to-right add of its REF cells (mean()'s order).
-    constexpr int E = MtdCfg<P>::E, NL = E + REF - 1;
+    constexpr int E = MtdCfg<P, BEAMS>::E, NL = E + REF - 1;
     const float* bl = mag + v0 - cv.save - REF;
     const float* br = mag + v0 + cv.save + 1;
     const float* bm = mag + v0;
@@ -1135,7 +1141,7 @@ struct MtdTile {
 template <int P, int REF, int BEAMS, int LA, int SA>
 __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem,
                                          uint32_t* s_hits) {
-    using C = MtdCfg<P>;
+    using C = MtdCfg<P, BEAMS>;
     constexpr int G = C::G, E = C::E, W = C::W;
     if (threadIdx.x == 0) *s_hits = 0u;   // published by the FFT's barriers
     const int c = threadIdx.x % W, g = threadIdx.x / W;
@@ -1215,7 +1221,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     o.lds_count = s_hits;
     o.cell0 = T.cell_base + (uint32_t)v0 * R + (uint32_t)r;
     if constexpr (REF > 0) {
-        doppler_cfar_fixed<P, REF>(mag, a.cv, col_on, v0, o);
+        doppler_cfar_fixed<P, REF, BEAMS>(mag, a.cv, col_on, v0, o);
     } else {
         float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
         doppler_sums(mag, sums, P, a.cv.ref, v0, v0 + E);
@@ -1247,7 +1253,7 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
         prev_chunk_hits(a);
         return;
     }
-    using C = MtdCfg<P>;
+    using C = MtdCfg<P, BEAMS>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_hits;
     const size_t cpi = blockIdx.y - yoff;
@@ -1386,7 +1392,7 @@ int mtd_bluestein_nf(int P) {
 template <int P, int REF, int BEAMS>
 static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                 const MtdArgs& a, hipStream_t s) {
-    using C = MtdCfg<P>;
+    using C = MtdCfg<P, BEAMS>;
     constexpr size_t lds = C::template lds_for<REF>();
     static bool attr_set = false;
     if (!attr_set) {
@@ -1404,7 +1410,7 @@ static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, in
 template <int P, int BEAMS = 1>
 static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                const MtdArgs& a, hipStream_t s) {
-    using C = MtdCfg<P>;
+    using C = MtdCfg<P, BEAMS>;
     // shift is 0 or floor(P/2) = G*E/2; the row rotation needs it to be a multiple of G,
     // and the padded sums column needs save + ref + 2 <= SPAD
     if (a.shift % C::G != 0 || a.shift < 0 || a.shift >= P) return hipErrorInvalidValue;
@@ -1415,26 +1421,38 @@ static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int
     return launch_mtd_pr<P, 0, BEAMS>(pc, rdm, flagV, ncpi, a, s);
 }
 
-template <int P>
-static void mtd_regions_p(int R_out, int ncpi, int* nregions, int* region) {
-    using C = MtdCfg<P>;
+// Hit-list regions of one MTD launch: one per workgroup (tile of W range bins), W * rows
+// entries each -- the tile's own cells, so a region can never overflow.
+template <int P, int BEAMS>
+static void mtd_regions_p(int rows, int R_out, int ncpi, int* nregions, int* region) {
+    using C = MtdCfg<P, BEAMS>;
     *nregions = ((R_out + C::W - 1) / C::W) * ncpi;
-    *region = C::W * P;
+    *region = C::W * rows;
 }
 
-void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region) {
+void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region, int beams) {
     *nregions = 0;
     *region = 0;
-    if (!mtd_size_supported(P, 1)) {   // Bluestein: NF-point tiles, P rows kept
-        const int nf = mtd_bluestein_nf(P);
-        if (!nf) return;
-        const int W = kBlock / (nf / 16);
-        *nregions = ((R_out + W - 1) / W) * ncpi;
-        *region = W * P;
+    if (beams == 1 && !mtd_size_supported(P, 1)) {   // Bluestein: NF-point tiles, P rows kept
+        switch (mtd_bluestein_nf(P)) {
+#define RSP_MB(nf) case nf: mtd_regions_p<nf, 1>(P, R_out, ncpi, nregions, region); break;
+            RSP_MB(64) RSP_MB(128) RSP_MB(256) RSP_MB(512) RSP_MB(1024) RSP_MB(2048)
+#undef RSP_MB
+            default: break;
+        }
+        return;
+    }
+    if (beams == 2) {
+        switch (P) {
+            case 512: mtd_regions_p<512, 2>(P, R_out, ncpi, nregions, region); break;
+            case 1024: mtd_regions_p<1024, 2>(P, R_out, ncpi, nregions, region); break;
+            case 2048: mtd_regions_p<2048, 2>(P, R_out, ncpi, nregions, region); break;
+            default: break;
+        }
         return;
     }
     switch (P) {
-#define RSP_MR(p) case p: mtd_regions_p<p>(R_out, ncpi, nregions, region); break;
+#define RSP_MR(p) case p: mtd_regions_p<p, 1>(P, R_out, ncpi, nregions, region); break;
         RSP_MR(16) RSP_MR(32) RSP_MR(64) RSP_MR(128) RSP_MR(256) RSP_MR(512) RSP_MR(1024)
         RSP_MR(2048) RSP_MR(48) RSP_MR(96) RSP_MR(192) RSP_MR(384) RSP_MR(768) RSP_MR(1536)
 #undef RSP_MR
