@@ -236,6 +236,52 @@ int rsp_set_fused(rsp_ctx* ctx, int32_t enable);
  * item (a bounded in-kernel wait that expired): RSP_ERR_HIP with a message if so. */
 int rsp_chain_check(rsp_ctx* ctx);
 
+/* ---- raw-data ingest --------------------------------------------------- */
+/* One frame of the radar's PRT record stream -> DBF beams, replacing the per-PRT loop of
+ *   [sig_data_DBF_allprts, servo_angle, frameCompleted, is_global_stream_end] =
+ *       FrameDataRead_xzr(orgDataFilePath, DBF_coeffs_data_C, Sig_Config, frameRInd)
+ * (FrameDataRead_xzr.m:20-204, called at bin_to_mat_xzr.m:62).  The host reads the frame's
+ * bytes from the cross-file stream (read_continuous_file_stream.m; rsp/ingest.py mirrors it)
+ * and this call parses and beamforms them on the GPU.  Record = head (bytes_head, uint32
+ * fields), realtime block, DDC payload int16 I/Q [sample][channel][I,Q] padded to 64 B, tail;
+ * every PRT of a frame has the same record size (rsp_ingest_record_bytes).
+ * Output: d_out[b * beam_stride + prt * point_prt + s] = sum_c (I + jQ)[s][c] * dbf[b][c]
+ * (sig_data_C * DBF_coeffs_data_C.', :158) as complex64, beam-major so each beam is the
+ * [prt][sample] echo the chain reads; beam_stride = 0 means prt_num * point_prt (pass a larger
+ * stride to land frames in a [beam][frames+1][P][R] window buffer).
+ * d_status: int32[prt_num + 1], per-PRT RSP_PRT_* codes, and [prt_num] = rows decoded: the
+ * frame stops at the first PRT the reference would return at (those rows and all later ones
+ * are written as zeros, servo 0), so frameCompleted == (status[prt_num] == prt_num && no
+ * RSP_PRT_TAIL_TRUNCATED).  Only DDC payloads (data_type 1) are built: ADC (type 0) cannot
+ * pass the reference's own size check with beam_num != channel_num, and its 24-bit DBF branch
+ * (type 2, :130-135) is marked unfinished there (uint8 arithmetic saturates). */
+typedef struct {
+    int32_t prt_num;         /* Sig_Config.prtNum (332) */
+    int32_t point_prt;       /* Sig_Config.point_PRT (3404) */
+    int32_t channel_num;     /* Sig_Config.channel_num (16) */
+    int32_t beam_num;        /* Sig_Config.beam_num (13) */
+    int32_t bytes_head;      /* Sig_Config.bytesFrameHead (64) */
+    int32_t bytes_realtime;  /* Sig_Config.bytesFrameRealtime (128) */
+    int32_t bytes_tail;      /* Sig_Config.bytesFrameEnd (64) */
+} rsp_ingest_params;
+
+enum {
+    RSP_PRT_OK = 0,
+    RSP_PRT_TRUNCATED = 1,        /* head, realtime block or payload cut by the end of the stream */
+    RSP_PRT_TAIL_TRUNCATED = 2,   /* decoded, but the tail is cut: the frame ends incomplete */
+    RSP_PRT_BAD_COUNT = 3,        /* pulse_data_num <= 0 (FrameDataRead_xzr.m:90-94) */
+    RSP_PRT_BAD_SHAPE = 4,        /* pulse_data_num != point_prt or channels != channel_num */
+    RSP_PRT_UNSUPPORTED_TYPE = 5  /* data_type != 1 (DDC) */
+};
+
+/* Bytes of one DDC PRT record of this shape. */
+int rsp_ingest_record_bytes(const rsp_ingest_params* p, int64_t* bytes);
+/* d_stream: nbytes of the frame's records (fewer than prt_num records: the rest are
+ * truncated); d_dbf: float32 [beam_num][channel_num][2] (re, im); d_servo nullable. */
+int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
+                       const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
+                       int32_t* d_status, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1

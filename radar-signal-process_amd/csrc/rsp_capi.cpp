@@ -1054,6 +1054,56 @@ int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t
     return RSP_OK;
 }
 
+// ------------------------------------------------------------------ raw-data ingest
+static int ingest_shape(rsp_ctx* ctx, const rsp_ingest_params* p, int64_t* rec) {
+    if (!p) return fail(ctx, RSP_ERR_ARG, "ingest: null params");
+    if (p->prt_num < 0 || p->point_prt <= 0 || p->channel_num <= 0 || p->channel_num > 255 || p->beam_num <= 0 ||
+        p->bytes_head < 64 || p->bytes_realtime < 0 || p->bytes_tail < 0 || p->bytes_head % 4 || p->bytes_realtime % 4)
+        return fail(ctx, RSP_ERR_ARG, "ingest: bad shape (prt %d, point %d, channels %d, beams %d, head %d)",
+                    p->prt_num, p->point_prt, p->channel_num, p->beam_num, p->bytes_head);
+    // FrameDataRead_xzr.m:108-119: DDC payload = samples * channels * 2 (I, Q) * 2 bytes, padded to 64 B
+    int64_t sig = (int64_t)p->point_prt * p->channel_num * 4;
+    if (sig % 64) sig += 64 - sig % 64;
+    if (sig >= 0x80000000ll) return fail(ctx, RSP_ERR_UNSUPPORTED, "ingest: payload of %lld bytes", (long long)sig);
+    *rec = (int64_t)p->bytes_head + p->bytes_realtime + sig + p->bytes_tail;
+    return RSP_OK;
+}
+
+int rsp_ingest_record_bytes(const rsp_ingest_params* p, int64_t* bytes) {
+    if (!bytes) return fail(nullptr, RSP_ERR_ARG, "rsp_ingest_record_bytes: null output");
+    return ingest_shape(nullptr, p, bytes);
+}
+
+int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
+                       const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
+                       int32_t* d_status, void* stream) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_ingest_ddc_dev: null ctx");
+    int64_t rec = 0;
+    int rc = ingest_shape(ctx, p, &rec);
+    if (rc) return rc;
+    if (!d_stream || nbytes < 0 || !d_dbf || !d_out || !d_status)
+        return fail(ctx, RSP_ERR_ARG, "rsp_ingest_ddc_dev: null buffer or negative byte count");
+    const int64_t plane = (int64_t)p->prt_num * p->point_prt;
+    if (beam_stride == 0) beam_stride = plane;
+    if (beam_stride < plane) return fail(ctx, RSP_ERR_ARG, "rsp_ingest_ddc_dev: beam_stride %lld < prt*point %lld",
+                                         (long long)beam_stride, (long long)plane);
+    if (p->prt_num == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    rsp::IngestArgs a{};
+    a.prt_num = p->prt_num;
+    a.point_prt = p->point_prt;
+    a.channel_num = p->channel_num;
+    a.beam_num = p->beam_num;
+    a.bytes_head = p->bytes_head;
+    a.bytes_realtime = p->bytes_realtime;
+    a.bytes_tail = p->bytes_tail;
+    a.rec_bytes = rec;
+    a.beam_stride = beam_stride;
+    HIP_TRY(ctx, rsp::launch_ingest_ddc(d_stream, nbytes, a, (const float2*)d_dbf, (float2*)d_out, d_servo, d_status,
+                                        (hipStream_t)stream));
+    return RSP_OK;
+}
+
 // ------------------------------------------------------------------ host-buffer entry points
 static size_t dtype_size(int32_t dtype) {
     switch (dtype) {

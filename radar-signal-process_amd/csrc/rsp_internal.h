@@ -116,6 +116,16 @@ struct MtdArgs {
     CfarRArgs prev_cr;
 };
 
+// Raw-data ingest (rsp_ingest.hip): one frame of uniform DDC PRT records.
+struct IngestArgs {
+    int prt_num, point_prt, channel_num, beam_num;
+    int bytes_head, bytes_realtime, bytes_tail;
+    int64_t rec_bytes;       // head + realtime + payload (padded to 64 B) + tail
+    int64_t beam_stride;     // output elements between consecutive beams' [prt][sample] planes
+};
+hipError_t launch_ingest_ddc(const uint8_t* stream, int64_t nbytes, const IngestArgs& a, const float2* dbf,
+                             float2* out, uint16_t* servo, int32_t* status, hipStream_t s);
+
 // The fused chain: PC -> MTD (+Doppler CFAR) -> range CFAR of a whole call in ONE launch
 // (chain_kernel).  CPI c belongs to work queue c % 8; queue h is a sequence of segments, and
 // segment s holds [PC items of the queue's CPI s][MTD tiles of CPI s-D][range-CFAR items of

@@ -29,7 +29,8 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
-           "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check")
+           "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check", "rsp_ingest_record_bytes",
+           "rsp_ingest_ddc_dev")
 RSP_NKERNELS = 5
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "chain_kernel")
 
@@ -64,6 +65,16 @@ class rsp_cfar_params(C.Structure):
                 ("nseg", C.c_int32),
                 ("seg_lo", C.c_int64 * RSP_MAX_SEG), ("seg_hi", C.c_int64 * RSP_MAX_SEG)]
 
+
+class rsp_ingest_params(C.Structure):
+    _fields_ = [("prt_num", C.c_int32), ("point_prt", C.c_int32), ("channel_num", C.c_int32),
+                ("beam_num", C.c_int32), ("bytes_head", C.c_int32), ("bytes_realtime", C.c_int32),
+                ("bytes_tail", C.c_int32)]
+
+
+# per-PRT ingest status codes (rsp_ingest_ddc_dev)
+(RSP_PRT_OK, RSP_PRT_TRUNCATED, RSP_PRT_TAIL_TRUNCATED, RSP_PRT_BAD_COUNT, RSP_PRT_BAD_SHAPE,
+ RSP_PRT_UNSUPPORTED_TYPE) = range(6)
 
 _lib = None
 
@@ -118,6 +129,10 @@ def load_library(path=None):
     lib.rsp_set_fused.argtypes = [vp, i32]
     lib.rsp_chain_check.restype = C.c_int
     lib.rsp_chain_check.argtypes = [vp]
+    lib.rsp_ingest_record_bytes.restype = C.c_int
+    lib.rsp_ingest_record_bytes.argtypes = [C.POINTER(rsp_ingest_params), C.POINTER(i64)]
+    lib.rsp_ingest_ddc_dev.restype = C.c_int
+    lib.rsp_ingest_ddc_dev.argtypes = [vp, vp, i64, C.POINTER(rsp_ingest_params), vp, vp, i64, vp, vp, vp]
     lib.rsp_profile.restype = C.c_int
     lib.rsp_profile.argtypes = [vp, i32]
     lib.rsp_profile_read.restype = C.c_int
