@@ -35,6 +35,8 @@ CONFIGS = {
     "c3": dict(P=128, R=4096, batch=1024, cfar=True, half=False, win=0),
     "c4": dict(P=256, R=8192, batch=32, cfar=True, half=False, win=4),
     "c5": dict(P=512, R=16384, batch=64, cfar=True, half=True, win=0),
+    # SURVEY.md §8f-2 (not a BASELINE config): raw PRT records -> DBF beams, v2 capture frames
+    "ingest": dict(P=332, R=3404, batch=8, cfar=False, half=False, win=0),
 }
 
 
@@ -109,6 +111,91 @@ def pmc_traffic(tag):
         return json.load(f)
 
 
+def bench_ingest(args, world, rank, local, dev, dist):
+    """--config ingest: frames/s through rsp_ingest_ddc_dev (record parse + DBF), v2 capture
+    frames (332 PRTs x 3404 samples x 16 channels int16 I/Q -> 13 beams complex64), records
+    resident in HBM; each rank decodes its own frames (no collective)."""
+    import torch
+    sys.path[:0] = [os.path.join(ROOT, "tests", "golden")]
+    from make_golden_ingest import synth_frame   # the synthetic record writer (test data only)
+    from rsp import ingest, shard
+    B = args.batch
+    lo, _ = shard.weak_shard(B, rank)
+    _, dbf, _, cfg, rec = synth_frame(args.P, args.R, 16, 13, seed=3000 + lo)
+    ing = ingest.Ingest(local)
+    d_rec = torch.frombuffer(bytearray(rec), dtype=torch.uint8).to(dev)
+    frames = d_rec.repeat(B)                          # B distinct frame slots of identical records
+    d_dbf = ing.dbf_device(dbf)
+    out = torch.empty((B, 13, args.P, args.R), dtype=torch.complex64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    nb = len(rec)
+
+    def step():
+        for f in range(B):
+            ing.decode_dev(frames[f * nb:(f + 1) * nb], nb, cfg, d_dbf, out=out[f], stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        # the fp64 oracle restatement of FrameDataRead_xzr.m on one host thread
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import ingest_ref
+        from threadpoolctl import threadpool_limits
+        done, t1 = 0, time.perf_counter()
+        with threadpool_limits(limits=1):
+            while time.perf_counter() - t1 < args.cpu_seconds or done == 0:
+                ingest_ref.FrameReader().read(ingest_ref.BytesStream(rec), dbf, cfg, 0)
+                done += 1
+        el = time.perf_counter() - t1
+        cpu = {"value": done / el, "unit": "frame/s", "cores": 1, "kind": "port",
+               "sample": "%d v2 capture frames in %.1f s: fp64 numpy restatement of FrameDataRead_xzr.m "
+                         "(record parse + DDC decode + DBF), BLAS limited to 1 thread" % (done, el)}
+    if rank == 0:
+        unit_bytes = nb + 13 * args.P * args.R * 8                 # records read + beams written
+        per_frame_s = gpu_ms / 1e3 / (args.steps * B)
+        ach = unit_bytes / per_frame_s / 1e9
+        print(json.dumps({
+            "metric": "frames/sec (v2 capture frame: 332 PRT x 3404 samples x 16 channels -> 13 DBF beams) "
+                      "through the record codec + DBF",
+            "value": round(world * B * args.steps / elapsed, 1), "unit": "frame/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16 in, f32",
+            "data": "synthetic PRT records (oracle/ingest_ref.prt_record format, seeded int16 I/Q)",
+            "config": {"workload": "ingest: %d frames per GPU per step, records resident in HBM" % B,
+                       "prt": args.P, "samples": args.R, "channels": 16, "beams": 13,
+                       "parallelism": "frame-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "kernel": "ingest_ddc_kernel", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": None, "alg_bytes_per_unit": unit_bytes,
+                         "avg_launch_us": round(per_frame_s * 1e6, 2),
+                         "note": "per-frame device time from events around the frame launches "
+                                 "(check + decode kernels)"},
+            "cpu_baseline": cpu}), flush=True)
+    ing.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     args.warmup = max(args.warmup, 1)
@@ -125,6 +212,8 @@ def main():
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.config == "ingest":
+        return bench_ingest(args, world, rank, local, dev, dist)
 
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)

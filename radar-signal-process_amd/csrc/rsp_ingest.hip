@@ -5,9 +5,9 @@
 // [beam][prt][sample] that the PC -> MTD chain reads.
 //
 // Two launches per frame, both on the caller's stream:
-//   ingest_check_kernel  one thread per PRT: validates its head against the frame shape
-//                        and the byte count, writes a status code, and folds the first
-//                        PRT the frame cannot get past into status[prt_num] (atomicMin);
+//   ingest_check_kernel  one workgroup, a thread per PRT: validates its head against the
+//                        frame shape and the byte count, writes a status code, and reduces
+//                        the first PRT the frame cannot get past into status[prt_num];
 //   ingest_ddc_kernel    one thread per (PRT, sample): 16-byte loads of the sample's
 //                        channel I/Q words, fp32 DBF with the coefficients read as scalars
 //                        (wave-uniform), one coalesced 8-byte store per beam; rows at or
@@ -29,42 +29,49 @@ namespace rsp {
 // per PRT, [7] data type (low 8) | PRT count (bits 8-23) | radar type (bits 24-31).
 constexpr int kHwChannels = 3, kHwServo = 4, kHwPulseDataNum = 6, kHwType = 7;
 
-__global__ __launch_bounds__(256) void ingest_check_kernel(const uint8_t* __restrict__ stream, int64_t nbytes,
-                                                            IngestArgs a, uint16_t* __restrict__ servo,
-                                                            int32_t* __restrict__ status) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.prt_num) return;
-    const int64_t base = (int64_t)p * a.rec_bytes;
-    int32_t st = RSP_PRT_OK;
-    int stop = a.prt_num;   // first row this PRT keeps from being decoded
-    if (base + a.bytes_head > nbytes) {
-        st = RSP_PRT_TRUNCATED;                      // :62-67
-        stop = p;
-    } else {
-        const uint32_t* h = reinterpret_cast<const uint32_t*>(stream + base);
-        const uint32_t pdn = h[kHwPulseDataNum];
-        const uint32_t ch = h[kHwChannels] & 0xffu;
-        const uint32_t type = h[kHwType] & 0xffu;
-        if ((int32_t)pdn <= 0) {
-            st = RSP_PRT_BAD_COUNT;                  // :90-94
+// One workgroup checks every PRT of the frame (a frame has a few hundred) and reduces the
+// stop row in LDS, so status[] needs no initialisation pass.
+__global__ __launch_bounds__(1024) void ingest_check_kernel(const uint8_t* __restrict__ stream, int64_t nbytes,
+                                                             IngestArgs a, uint16_t* __restrict__ servo,
+                                                             int32_t* __restrict__ status) {
+    __shared__ int s_stop;
+    if (threadIdx.x == 0) s_stop = a.prt_num;
+    __syncthreads();
+    for (int p = threadIdx.x; p < a.prt_num; p += blockDim.x) {
+        const int64_t base = (int64_t)p * a.rec_bytes;
+        int32_t st = RSP_PRT_OK;
+        int stop = a.prt_num;   // first row this PRT keeps from being decoded
+        if (base + a.bytes_head > nbytes) {
+            st = RSP_PRT_TRUNCATED;                      // :62-67
             stop = p;
-        } else if (type != 1u) {
-            st = RSP_PRT_UNSUPPORTED_TYPE;           // ADC / DBF payloads: not built
-            stop = p;
-        } else if ((int)ch != a.channel_num || (int)pdn != a.point_prt) {
-            st = RSP_PRT_BAD_SHAPE;                  // :171-176 (and the DBF product's inner dimension)
-            stop = p;
-        } else if (base + a.rec_bytes - a.bytes_tail > nbytes) {
-            st = RSP_PRT_TRUNCATED;                  // realtime block or payload cut (:97-127)
-            stop = p;
-        } else if (base + a.rec_bytes > nbytes) {
-            st = RSP_PRT_TAIL_TRUNCATED;             // stored, then the tail read fails (:179-189)
-            stop = p + 1;
+        } else {
+            const uint32_t* h = reinterpret_cast<const uint32_t*>(stream + base);
+            const uint32_t pdn = h[kHwPulseDataNum];
+            const uint32_t ch = h[kHwChannels] & 0xffu;
+            const uint32_t type = h[kHwType] & 0xffu;
+            if ((int32_t)pdn <= 0) {
+                st = RSP_PRT_BAD_COUNT;                  // :90-94
+                stop = p;
+            } else if (type != 1u) {
+                st = RSP_PRT_UNSUPPORTED_TYPE;           // ADC / DBF payloads: not built
+                stop = p;
+            } else if ((int)ch != a.channel_num || (int)pdn != a.point_prt) {
+                st = RSP_PRT_BAD_SHAPE;                  // :171-176 (and the DBF product's inner dimension)
+                stop = p;
+            } else if (base + a.rec_bytes - a.bytes_tail > nbytes) {
+                st = RSP_PRT_TRUNCATED;                  // realtime block or payload cut (:97-127)
+                stop = p;
+            } else if (base + a.rec_bytes > nbytes) {
+                st = RSP_PRT_TAIL_TRUNCATED;             // stored, then the tail read fails (:179-189)
+                stop = p + 1;
+            }
+            if (servo) servo[p] = (uint16_t)(h[kHwServo] & 0xffffu);   // zeroed below for rows past the stop
         }
-        if (servo) servo[p] = (uint16_t)(h[kHwServo] & 0xffffu);   // zeroed below for rows past the stop
+        status[p] = st;
+        if (stop < a.prt_num) atomicMin(&s_stop, stop);
     }
-    status[p] = st;
-    if (stop < a.prt_num) atomicMin(&status[a.prt_num], stop);
+    __syncthreads();
+    if (threadIdx.x == 0) status[a.prt_num] = s_stop;
 }
 
 // out[b * beam_stride + p * point + s] = sum_c (I_c + j Q_c) * C[b][c], fp32 in channel order.
@@ -135,14 +142,9 @@ __global__ __launch_bounds__(256) void ingest_ddc_kernel(const uint8_t* __restri
 hipError_t launch_ingest_ddc(const uint8_t* stream, int64_t nbytes, const IngestArgs& a, const float2* dbf,
                              float2* out, uint16_t* servo, int32_t* status, hipStream_t s) {
     if (a.prt_num <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(status, 0, (size_t)a.prt_num * sizeof(int32_t), s);
+    hipLaunchKernelGGL(ingest_check_kernel, dim3(1), dim3(1024), 0, s, stream, nbytes, a, servo, status);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // status[prt_num] = rows decoded: prt_num unless a PRT lowers it
-    e = hipMemsetD32Async((hipDeviceptr_t)(status + a.prt_num), a.prt_num, 1, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ingest_check_kernel, dim3((a.prt_num + 255) / 256), dim3(256), 0, s, stream, nbytes, a, servo,
-                       status);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     const dim3 grid((unsigned)((a.point_prt + 255) / 256), (unsigned)a.prt_num);
     if (a.channel_num == 16 && a.beam_num == 13)   // the v2 capture (bin_to_mat_xzr.m:39-40)
         hipLaunchKernelGGL((ingest_ddc_kernel<16, 13>), grid, dim3(256), 0, s, stream, a, dbf, out, servo, status);
