@@ -942,7 +942,10 @@ struct MtdCfg {
 #ifndef RSP_MTD_WIDE
 #define RSP_MTD_WIDE 1
 #endif
-    static constexpr int E = (P % 3 == 0) ? 24 : ((RSP_MTD_WIDE && BEAMS == 1 && P >= 512) ? 32 : 16);
+#ifndef RSP_MTD_E_SMALL
+#define RSP_MTD_E_SMALL 16   // elements per thread for 2^k lengths below 512 (A/B knob)
+#endif
+    static constexpr int E = (P % 3 == 0) ? 24 : ((RSP_MTD_WIDE && BEAMS == 1 && P >= 512) ? 32 : RSP_MTD_E_SMALL);
     static constexpr int G = P / E;                    // threads per range bin
     static constexpr int W = kBlock / G;               // range bins per workgroup
     static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
@@ -1138,13 +1141,34 @@ struct MtdTile {
 
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
-template <int P, int REF, int BEAMS, int LA, int SA>
+// The raw PC samples of one single-beam tile: lane (c, g) loads rows g + G*m of range bin c.
+template <int P, int LA, int E>
+__device__ __forceinline__ void mtd_tile_load(float2 (&v)[E], const float2* pc, int bx, const MtdArgs& a,
+                                              bool valid) {
+    using C = MtdCfg<P, 1>;
+    static_assert(E == C::E, "tile shape");
+    constexpr int G = C::G, W = C::W;
+    const int c = threadIdx.x % W, g = threadIdx.x / W;
+    const uint32_t R = (uint32_t)a.R_out;
+    const int r = bx * W + c;
+    const uint32_t vo_in = (valid && r < (int)R) ? ((uint32_t)g * R + (uint32_t)r) * 8u : kOob;
+    const auto src = buf_rsrc(pc, (uint32_t)a.pin * R * 8u);
+#pragma unroll
+    for (int m = 0; m < E; ++m) v[m] = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
+}
+
+// PRE: the tile's samples were loaded ahead (mtd_tile_load into `pre`, single beam).
+template <int P, int REF, int BEAMS, int LA, int SA, bool PRE = false>
 __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem,
-                                         uint32_t* s_hits) {
+                                         uint32_t* s_hits, const float2* pre = nullptr) {
     using C = MtdCfg<P, BEAMS>;
     constexpr int G = C::G, E = C::E, W = C::W;
     if (threadIdx.x == 0) *s_hits = 0u;   // published by the FFT's barriers
-    const int c = threadIdx.x % W, g = threadIdx.x / W;
+    // persistent use (PRE): an opaque copy of the thread index, so the tile's lane-derived
+    // addresses, window and twiddle loads are not hoisted out of the tile loop (and spilled)
+    int tx = threadIdx.x;
+    if constexpr (PRE) asm volatile("" : "+v"(tx));
+    const int c = tx % W, g = tx / W;
     const uint32_t R = (uint32_t)a.R_out;
     const int r = T.bx * W + c;
     const bool rv = r < (int)R;
@@ -1159,7 +1183,9 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         const auto src = buf_rsrc(T.pc + (size_t)b * pin * R, (uint32_t)pin * R * 8u);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float2 v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
+            float2 v;
+            if constexpr (PRE) v = pre[m];
+            else v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
             const float w = a.win[g + G * m];
             u[m] = make_float2(v.x * w, v.y * w);
         }
@@ -1169,6 +1195,25 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 #pragma unroll
                 for (int m = 0; m < E; ++m) m0[m] = __builtin_amdgcn_sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
             }
+        }
+    }
+
+    // The flag plane's zero background for this tile (range stage on: the 1s come later from
+    // the hit list): W columns x P rows, one 16-byte store per row segment, issued while the
+    // FFT runs -- instead of a byte store per cell in the Doppler epilogue.
+    bool bg_done = false;
+    if constexpr (W % 16 == 0) {
+        if (T.flag && a.cv.enabled && a.rflag && a.flag_zero && (R % 16u) == 0u) {
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            const auto fz = buf_rsrc(T.flag, plane);
+            constexpr int SEG = W / 16;
+            for (int i = threadIdx.x; i < P * SEG; i += kBlock) {
+                const int c0 = T.bx * W + (i % SEG) * 16;
+                if (c0 < (int)R)
+                    __builtin_amdgcn_raw_buffer_store_b128(v4i{0, 0, 0, 0}, fz, (uint32_t)(i / SEG) * R + (uint32_t)c0,
+                                                           0u, 0);
+            }
+            bg_done = true;
         }
     }
 
@@ -1212,7 +1257,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     o.want_fv = T.flagV != nullptr;
     o.fused = T.flag != nullptr;
     o.rflag = a.rflag != 0;
-    o.zero_bg = a.flag_zero != 0;
+    o.zero_bg = a.flag_zero != 0 && !bg_done;
     o.fv = buf_rsrc(o.want_fv ? T.flagV : nullptr, o.want_fv ? plane : 0u);
     o.fl = buf_rsrc(o.fused ? T.flag : nullptr, o.fused ? plane : 0u);
     o.vo = rv ? (uint32_t)v0 * R + (uint32_t)r : kOob;
@@ -1273,6 +1318,74 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
     mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
+}
+
+// Persistent single-beam MTD (RSP_MTD_PERSIST=1; off: 1.42 vs 1.15 us/CPI for MTD alone at c3,
+// the hardware's workgroup scheduling overlaps tiles better): a resident grid walks the launch's tiles (tile = cpi * nbx + bx,
+// the hit-list region of mtd_kernel's workgroup of the same tile), and each workgroup loads
+// its next tile's samples before it runs the current one's FFT and Doppler CFAR -- the CFAR
+// phase otherwise leaves the workgroup with no memory in flight.  Blocks [0, nprev) run the
+// previous chunk's range stage (dispatched first, as mtd_kernel's row 0).
+#ifndef RSP_MTD_PERSIST
+#define RSP_MTD_PERSIST 0   // measured slower than the one-tile-per-workgroup mtd_kernel
+#endif
+__device__ __forceinline__ void prev_chunk_hits_b(const MtdArgs& a, int b, int nb) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kBlock / 64;
+    const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
+    for (int rg = b * nw + w; rg < a.prev_nregions; rg += nb * nw) {
+        if (ref57)
+            cfar_hit_region<5, 7>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
+                                  lane);
+        else
+            cfar_hit_region<0, 0>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
+                                  lane);
+    }
+}
+
+template <int P, int REF>
+__global__ __launch_bounds__(kBlock, 4) void mtd_persist_kernel(const float2* __restrict__ pc, float* __restrict__ rdm,
+                                                             uint8_t* __restrict__ flagV, MtdArgs a, int ntiles,
+                                                             int nbx, int nprev) {
+    if ((int)blockIdx.x < nprev) {
+        prev_chunk_hits_b(a, blockIdx.x, nprev);
+        return;
+    }
+    using C = MtdCfg<P, 1>;
+    constexpr int E = C::E;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_hits;
+    const int nwg = (int)gridDim.x - nprev;
+    int t = (int)blockIdx.x - nprev;
+    if (t >= ntiles) return;
+    const size_t R = (size_t)a.R_out;
+    const size_t plane = (size_t)P * R;
+    auto rows = [&](int tile) {   // first PC row of the tile's CPI
+        const size_t cpi = (size_t)(tile / nbx);
+        return a.nwin > 0 ? (cpi / a.nwin) * (size_t)a.pin + a.win_start[cpi % a.nwin] : cpi * (size_t)a.pin;
+    };
+    float2 u[E];
+    mtd_tile_load<P, 0>(u, pc + rows(t) * R, t % nbx, a, true);
+    while (t < ntiles) {
+        const int tn = t + nwg;
+        float2 nx[E];   // the next tile, in flight during this one
+        mtd_tile_load<P, 0>(nx, pc + rows(tn < ntiles ? tn : t) * R, (tn < ntiles ? tn : t) % nbx, a, tn < ntiles);
+        const size_t cpi = (size_t)(t / nbx);
+        MtdTile T;
+        T.pc = pc + rows(t) * R;
+        T.rdm = rdm + cpi * plane;
+        T.diff = nullptr;
+        T.flagV = flagV ? flagV + cpi * plane : nullptr;
+        T.flag = a.flag ? a.flag + cpi * plane : nullptr;
+        T.hits = a.hits ? a.hits + (size_t)t * (C::W * P) : nullptr;
+        T.hit_count = a.hit_count ? a.hit_count + t : nullptr;
+        T.cell_base = (uint32_t)(cpi * plane);
+        T.bx = t % nbx;
+        mtd_tile<P, REF, 1, 0, 0, true>(T, a, smem, &s_hits, u);
+        __syncthreads();   // the tile's last LDS reads (CFAR) and s_hits store are done
+#pragma unroll
+        for (int m = 0; m < E; ++m) u[m] = nx[m];
+        t = tn;
+    }
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
@@ -1389,11 +1502,38 @@ int mtd_bluestein_nf(int P) {
     return nf <= 2048 ? nf : 0;
 }
 
+template <int P, int REF>
+static hipError_t launch_mtd_persist(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
+                                     hipStream_t s) {
+    using C = MtdCfg<P, 1>;
+    constexpr size_t lds = C::template lds_for<REF>();
+    static int resident = 0;
+    if (!resident) {
+        hipError_t e = hipFuncSetAttribute((const void*)mtd_persist_kernel<P, REF>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mtd_persist_kernel<P, REF>, kBlock, lds);
+        if (e != hipSuccess) return e;
+        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
+    }
+    const int nbx = (a.R_out + C::W - 1) / C::W;
+    const int ntiles = nbx * ncpi;
+    const int nprev = a.prev_nregions > 0 ? nbx : 0;
+    const int nwg = ntiles < resident ? ntiles : resident;
+    if (nwg + nprev < 1) return hipSuccess;
+    hipLaunchKernelGGL((mtd_persist_kernel<P, REF>), dim3((unsigned)(nwg + nprev)), dim3(kBlock), lds, s, pc, rdm,
+                       flagV, a, ntiles, nbx, nprev);
+    return hipGetLastError();
+}
+
 template <int P, int REF, int BEAMS>
 static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                 const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P, BEAMS>;
     constexpr size_t lds = C::template lds_for<REF>();
+    if constexpr (RSP_MTD_PERSIST && BEAMS == 1 && C::E == 16)
+        return launch_mtd_persist<P, REF>(pc, rdm, flagV, ncpi, a, s);
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P, REF, BEAMS>,
