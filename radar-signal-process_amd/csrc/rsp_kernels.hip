@@ -173,6 +173,9 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // 256..512-thread workgroup.  Row loads and stores are lane-contiguous (the strided
 // element pattern of fft_reg), the spectrum multiply sits between the forward and the
 // inverse FFT in registers, and the only LDS traffic is the inter-pass exchange.
+#ifndef RSP_PC_WIDE_N
+#define RSP_PC_WIDE_N 16384
+#endif
 #ifndef RSP_PC_E
 #define RSP_PC_E 16
 #endif
@@ -181,7 +184,9 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #endif
 template <int N>
 struct PcCfg {
-    static constexpr int G = N / RSP_PC_E;                      // threads per row
+    // 16 elements per thread; 32 from 16384 points on, so a row is 512 threads (2 waves per
+    // SIMD, a 256-VGPR budget) instead of 1024 (128 VGPRs: the preloaded twiddles spill)
+    static constexpr int G = N / (N >= RSP_PC_WIDE_N ? 32 : RSP_PC_E);   // threads per row
     static constexpr int E = N / G;                             // elements per thread
     static constexpr int RPB = G >= 256 ? 1 : 256 / G;          // rows per workgroup
     static constexpr int T = G * RPB;
