@@ -468,6 +468,9 @@ __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, flo
 #ifndef RSP_PC_LEAN
 #define RSP_PC_LEAN 0
 #endif
+#ifndef RSP_PC_PER_CU
+#define RSP_PC_PER_CU 0   // persistent PC workgroups per CU (0: as many as fit)
+#endif
 #ifndef RSP_PERSIST_WAVES
 #define RSP_PERSIST_WAVES (RSP_PC_LEAN ? 4 : 2)
 #endif
@@ -748,6 +751,7 @@ static hipError_t launch_pc_persist(const TIn* echo, float2* out, const PcMfArgs
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_persist_kernel<TIn, N1, N2>,
                                                          PC::T, PC::lds);
         if (e != hipSuccess) return e;
+        if (RSP_PC_PER_CU > 0 && RSP_PC_PER_CU < per_cu) per_cu = RSP_PC_PER_CU;   // A/B: leave CU room to MTD
         resident = (per_cu > 0 ? per_cu : 1) * device_cus();
     }
     const int n2 = a1.rows;                                  // one item per long-segment row
@@ -815,6 +819,9 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
 #ifndef RSP_PC_PERSIST
 #define RSP_PC_PERSIST 1
 #endif
+#ifndef RSP_PC_PERSIST8K
+#define RSP_PC_PERSIST8K 1   // the persistent kernel for the 1024 + 8192 pair (c4: PC 314 -> 185 us per launch)
+#endif
 #if RSP_PC_WAVE
 #define RSP_PC_WAVE_LAUNCH(n1, n2) if (n2 == 4096) return launch_pc_wave<TIn, n1>(echo, out, a1, *a2, s);
 #else
@@ -835,7 +842,11 @@ static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a
     // fused pairs of the built-in presets (v2 at 1024..16384 range bins, legacy)
     RSP_PAIR(1024, 1024);
     RSP_PAIR_PERSIST(1024, 4096);
+#if RSP_PC_PERSIST8K
+    RSP_PAIR_PERSIST(1024, 8192);
+#else
     RSP_PAIR(1024, 8192);
+#endif
     RSP_PAIR(1024, 16384);
     RSP_PAIR(512, 1024);
     if (a2) return hipErrorNotSupported;
