@@ -963,7 +963,13 @@ struct MtdCfg {
 #endif
     static constexpr int E = (P % 3 == 0) ? 24 : ((RSP_MTD_WIDE && BEAMS == 1 && P >= 512) ? 32 : RSP_MTD_E_SMALL);
     static constexpr int G = P / E;                    // threads per range bin
-    static constexpr int W = kBlock / G;               // range bins per workgroup
+    // threads per workgroup: 512 for one-beam P = 256 (32 range bins, 256-B row segments, at
+    // the same LDS per range bin), 256 otherwise
+#ifndef RSP_MTD_WIDE256
+#define RSP_MTD_WIDE256 0   // measured neutral at c4 (529 vs 523 us per launch)
+#endif
+    static constexpr int T = (RSP_MTD_WIDE256 && BEAMS == 1 && P == 256) ? 512 : kBlock;
+    static constexpr int W = T / G;                    // range bins per workgroup
     static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
     static constexpr int MS = P + 1;                   // odd float stride of a CFAR column
     static constexpr int SPAD = 32;                    // sums pad: save + ref + 2 <= 32 (host-checked)
@@ -978,7 +984,7 @@ struct MtdCfg {
     static constexpr size_t lds_reg = lds_fft > lds_cfar_reg ? lds_fft : lds_cfar_reg;
     template <int REF>
     static constexpr size_t lds_for() { return REF > 0 ? lds_reg : lds; }
-    static_assert(G * E == P && (G & (G - 1)) == 0 && G <= kBlock, "MTD tiling");
+    static_assert(G * E == P && (G & (G - 1)) == 0 && G <= T, "MTD tiling");
 };
 
 // Per-row outputs of the Doppler CFAR at cell (v, r) of launch CPI `cpi`: flagV (if requested),
@@ -1120,7 +1126,7 @@ __device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, u
 // The previous chunk's range stage inside an MTD launch: the extra row of workgroups
 // (blockIdx.y == gridDim.y - 1), one wave per hit region.
 __device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kBlock / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (int)blockDim.x / 64;
     const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
     for (int rg = blockIdx.x * nw + w; rg < a.prev_nregions; rg += gridDim.x * nw) {
         if (ref57)
@@ -1223,7 +1229,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             typedef int v4i __attribute__((ext_vector_type(4)));
             const auto fz = buf_rsrc(T.flag, plane);
             constexpr int SEG = W / 16;
-            for (int i = threadIdx.x; i < P * SEG; i += kBlock) {
+            for (int i = threadIdx.x; i < P * SEG; i += C::T) {
                 const int c0 = T.bx * W + (i % SEG) * 16;
                 if (c0 < (int)R)
                     __builtin_amdgcn_raw_buffer_store_b128(v4i{0, 0, 0, 0}, fz, (uint32_t)(i / SEG) * R + (uint32_t)c0,
@@ -1306,7 +1312,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 // the zero padding of fft(x, P, 1): out of the buffer's range, they load as 0).  BEAMS == 2:
 // the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
 template <int P, int REF, int BEAMS>
-__global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ pc,
+__global__ __launch_bounds__((MtdCfg<P, BEAMS>::T)) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
     const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
@@ -1346,7 +1352,7 @@ __global__ __launch_bounds__(kBlock) void mtd_kernel(const float2* __restrict__ 
 #define RSP_MTD_PERSIST 0   // measured slower than the one-tile-per-workgroup mtd_kernel
 #endif
 __device__ __forceinline__ void prev_chunk_hits_b(const MtdArgs& a, int b, int nb) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kBlock / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (int)blockDim.x / 64;
     const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
     for (int rg = b * nw + w; rg < a.prev_nregions; rg += nb * nw) {
         if (ref57)
@@ -1359,7 +1365,7 @@ __device__ __forceinline__ void prev_chunk_hits_b(const MtdArgs& a, int b, int n
 }
 
 template <int P, int REF>
-__global__ __launch_bounds__(kBlock, 4) void mtd_persist_kernel(const float2* __restrict__ pc, float* __restrict__ rdm,
+__global__ __launch_bounds__((MtdCfg<P>::T), 4) void mtd_persist_kernel(const float2* __restrict__ pc, float* __restrict__ rdm,
                                                              uint8_t* __restrict__ flagV, MtdArgs a, int ntiles,
                                                              int nbx, int nprev) {
     if ((int)blockIdx.x < nprev) {
@@ -1412,7 +1418,7 @@ __global__ __launch_bounds__(kBlock, 4) void mtd_persist_kernel(const float2* __
 // needs no final chirp.  Bins k < P are kept; fftshift / 0-v / Doppler CFAR as mtd_kernel
 // (runtime CFAR window), with per-element row offsets (P is not a multiple of G).
 template <int NF>
-__global__ __launch_bounds__(kBlock) void mtd_bluestein_kernel(const float2* __restrict__ pc,
+__global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const float2* __restrict__ pc,
                                                                float* __restrict__ rdm,
                                                                uint8_t* __restrict__ flagV, MtdArgs a) {
     const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
@@ -1507,7 +1513,7 @@ static hipError_t launch_mtd_bluestein(const float2* pc, float* rdm, uint8_t* fl
         attr_set = true;
     }
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
-        block(kBlock);
+        block(C::T);
     hipLaunchKernelGGL((mtd_bluestein_kernel<NF>), grid, block, C::lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
@@ -1529,7 +1535,7 @@ static hipError_t launch_mtd_persist(const float2* pc, float* rdm, uint8_t* flag
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         int per_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mtd_persist_kernel<P, REF>, kBlock, lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mtd_persist_kernel<P, REF>, C::T, lds);
         if (e != hipSuccess) return e;
         resident = (per_cu > 0 ? per_cu : 1) * device_cus();
     }
@@ -1538,7 +1544,7 @@ static hipError_t launch_mtd_persist(const float2* pc, float* rdm, uint8_t* flag
     const int nprev = a.prev_nregions > 0 ? nbx : 0;
     const int nwg = ntiles < resident ? ntiles : resident;
     if (nwg + nprev < 1) return hipSuccess;
-    hipLaunchKernelGGL((mtd_persist_kernel<P, REF>), dim3((unsigned)(nwg + nprev)), dim3(kBlock), lds, s, pc, rdm,
+    hipLaunchKernelGGL((mtd_persist_kernel<P, REF>), dim3((unsigned)(nwg + nprev)), dim3(C::T), lds, s, pc, rdm,
                        flagV, a, ntiles, nbx, nprev);
     return hipGetLastError();
 }
@@ -1558,7 +1564,7 @@ static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, in
         attr_set = true;
     }
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
-        block(kBlock);
+        block(C::T);
     hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
