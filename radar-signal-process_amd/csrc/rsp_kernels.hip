@@ -449,6 +449,9 @@ __device__ __forceinline__ void mf_store(const float2 (&u)[N / G], float2* __res
     for (int m = 0; m < N / G; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
 }
 
+#ifndef RSP_PC_SHORT_WS
+#define RSP_PC_SHORT_WS 1
+#endif
 // The short-segment groups of a persistent PC workgroup: items first, +gridDim.x, ... < nitems.
 template <typename TIn, int N1, int N2>
 __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, float2* __restrict__ out,
@@ -459,9 +462,14 @@ __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, flo
     using PC = PairCfg<N1, N2>;
     constexpr int G1 = PcCfg<N1>::G;
     const int grp = threadIdx.x / G1, t1 = threadIdx.x % G1;
+    // G1 == 64: a short row is one wave with its own LDS slot, so its exchanges need only the
+    // wave's own ordering (RSP_PC_SHORT_WS): the four rows of a group no longer wait for each
+    // other at every FFT pass
+    constexpr bool WS = RSP_PC_SHORT_WS && G1 == 64;
+    if constexpr (WS) __syncthreads();   // the long rows' last LDS reads are done
     for (int item = first; item < nitems; item += (int)gridDim.x) {
-        __syncthreads();   // the previous item's last LDS reads are done
-        pc_row<TIn, N1, G1>(echo, out, a1, (item - n2) * PC::RPB1 + grp, t1, lds + grp * PcCfg<N1>::SLOT);
+        if constexpr (!WS) __syncthreads();   // the previous item's last LDS reads are done
+        pc_row<TIn, N1, G1, 0, WS>(echo, out, a1, (item - n2) * PC::RPB1 + grp, t1, lds + grp * PcCfg<N1>::SLOT);
     }
 }
 
