@@ -282,6 +282,40 @@ int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, co
                        const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
                        int32_t* d_status, void* stream);
 
+/* ---- post-detection measurement --------------------------------------- */
+/* Range / velocity / elevation of every CFAR hit, replacing
+ *   [rEstSeries, vEstSeries, eleAngleEstSeries] = motionParaMeasure(echo_MTD_sum, echo_MTD_diff,
+ *       cfarResultFlag, extraDots, rScale, deltaR, rInterpTimes, vScale, deltaV, vInterpTimes,
+ *       kValues, beamPosNum, beamAngleStep, freInd, eleAngleComp, eleAngleSysErr, MTD_0_num)
+ * (MatlabProcess_xuzerui/CFAR_WangCai/motionParaMeasure.m:1-88, called at
+ * DMX_SignalProcessing_main_xzr.m:489-494) for a batch of CPIs.  d_sum / d_diff: float32
+ * [batch][V][R] (rsp_pc_mtd_cfar_diff_dev's d_sum / d_diff), d_flag: uint8 [batch][V][R]
+ * (its d_flag); d_r_scale: float64 [R] (rScale), d_v_scale: float64 [V] (vScale).
+ * Hit i of a CPI, in MATLAB's find() order (column-major: range bin, then Doppler row), gets
+ * d_est[(cpi*max_hits + i)*3 + {0,1,2}] = {rEst, vEst, eleAngleEst} (float64) and, when
+ * d_cells != NULL, d_cells[(cpi*max_hits + i)*2 + {0,1}] = its 0-based (row, column).
+ * d_count[cpi*2] = hits in the CPI (only the first max_hits are written), d_count[cpi*2+1] =
+ * hits the reference stops at with an index error (a hit too close to an edge for the
+ * re-anchoring at :24-32 / :51-59); their estimates are NaN. */
+typedef struct {
+    int32_t extra_dots;      /* extraDots (2), 1..4: 2*extraDots+1 cells per spline */
+    int32_t r_interp;        /* rInterpTimes (8), 1..64 */
+    int32_t v_interp;        /* vInterpTimes (4), 1..64 */
+    int32_t mtd0_num;        /* MTD_0_num: rows 1..M0+1 and V-M0+1..V are clutter-zeroed */
+    int32_t beam_pos_num;    /* beamPosNum */
+    double delta_r;          /* deltaR [m] */
+    double delta_v;          /* deltaV [m/s] */
+    double k_value;          /* kValues(freInd+1, beamPosNum+1) (angle_KvalueGen.m) */
+    double beam_angle_step;  /* beamAngleStep [deg] (5) */
+    double ele_comp;         /* eleAngleComp */
+    double ele_sys_err;      /* eleAngleSysErr */
+} rsp_measure_params;
+
+int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff, const uint8_t* d_flag,
+                           int64_t V, int64_t R, int64_t batch, const rsp_measure_params* mp,
+                           const double* d_r_scale, const double* d_v_scale, int64_t max_hits,
+                           double* d_est, int32_t* d_cells /* nullable */, int32_t* d_count, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1

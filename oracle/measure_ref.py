@@ -1,0 +1,165 @@
+"""oracle/measure_ref.py -- TEST INFRASTRUCTURE ONLY.
+
+fp64 restatement of the reference's post-detection measurement, the
+checker of the HIP path in radar-signal-process_amd/csrc/rsp_measure.hip:
+
+  * MatlabProcess_xuzerui/CFAR_WangCai/motionParaMeasure.m:1-88 -- for every CFAR hit, in
+    MATLAB's column-major find() order (:6): range and velocity refined by a not-a-knot
+    cubic spline (interp1 'spline', :38,:65) over 2*extraDots+1 cells around the hit, moved
+    inside the matrix edges (:24-32) and outside the zeroed clutter rows (:51-59), queried at
+    1/interpTimes steps (:37,:64) with the first maximum taken (:39-42,:66-69); elevation
+    from the sum/difference amplitude ratio and the K-value table (:76-79);
+  * CFAR_WangCai/angle_KvalueGen.m and freValueGen.m: table lookups, done by the caller.
+
+MATLAB's `spline` with n >= 4 points and the not-a-knot end conditions is the unique cubic
+spline whose third derivative is continuous at the second and the second-to-last knot; with
+3 points it is the interpolating parabola.  It is restated here on second derivatives with
+unit knot spacing: the two end conditions turn the first and last interior rows into
+6*M_1 = d_1 and 6*M_{n-2} = d_{n-2} (d_i = 6*second difference), the rows between are a
+tridiagonal solve, and M_0 / M_{n-1} follow by linear extrapolation.  The tests check this
+against scipy's CubicSpline(bc_type='not-a-knot'), an independent implementation of the
+same published definition.  The query abscissae follow MATLAB's colon for a:d:b (first half
+a + i*d, second half b - (n-1-i)*d), which is exact for the reference's interpolation factors
+(8 and 4, DMX_SignalProcessing_main_xzr.m:257-258).
+
+Where the reference raises an error (a hit too close to an edge for its re-anchoring, :25,
+:30, :52, :57, or an index outside the matrix) this module raises IndexError.  Parity is
+"unpinned" beyond this restatement: the reference ships no measurement outputs.  Nothing in
+the product imports this module.
+"""
+import math
+
+import numpy as np
+
+
+def colon(a, d, b):
+    """MATLAB a:d:b for d > 0 (elements a + i*d in the first half, b - (n-1-i)*d in the
+    second, so the last element is b exactly when (b - a)/d is an integer)."""
+    n = int(math.floor((b - a) / d + 1e-10)) + 1
+    out = np.empty(n)
+    for i in range(n):
+        out[i] = a + i * d if 2 * i < n else b - (n - 1 - i) * d
+    return out
+
+
+def spline_m(y):
+    """Second derivatives of the not-a-knot cubic spline through y at knots 0..n-1."""
+    y = np.asarray(y, dtype=np.float64)
+    n = len(y)
+    if n < 3:
+        raise ValueError("spline needs at least 3 points here")
+    m = np.zeros(n)
+    if n == 3:
+        m[:] = y[2] - 2 * y[1] + y[0]
+        return m
+    d = 6.0 * (y[2:] - 2.0 * y[1:-1] + y[:-2])          # d[i-1] for interior row i = 1..n-2
+    m[1] = d[0] / 6.0
+    m[n - 2] = d[n - 3] / 6.0
+    k = n - 4                                            # unknowns M_2 .. M_{n-3}
+    if k > 0:
+        rhs = d[1:n - 3].copy()
+        rhs[0] -= m[1]
+        rhs[-1] -= m[n - 2]
+        # Thomas algorithm on the (1, 4, 1) rows
+        c = np.zeros(k)
+        g = np.zeros(k)
+        c[0] = 1.0 / 4.0
+        g[0] = rhs[0] / 4.0
+        for i in range(1, k):
+            den = 4.0 - c[i - 1]
+            c[i] = 1.0 / den
+            g[i] = (rhs[i] - g[i - 1]) / den
+        x = np.zeros(k)
+        x[-1] = g[-1]
+        for i in range(k - 2, -1, -1):
+            x[i] = g[i] - c[i] * x[i + 1]
+        m[2:n - 2] = x
+    m[0] = 2.0 * m[1] - m[2]
+    m[n - 1] = 2.0 * m[n - 2] - m[n - 3]
+    return m
+
+
+def spline_eval(y, m, t):
+    """Value of the spline (y, m) at t in [0, n-1]; interval j = floor(t) clamped to n-2."""
+    n = len(y)
+    j = min(max(int(math.floor(t)), 0), n - 2)
+    u = t - j
+    w = 1.0 - u
+    return w * y[j] + u * y[j + 1] + ((w * w * w - w) * m[j] + (u * u * u - u) * m[j + 1]) / 6.0
+
+
+def fix_cells(center, e, lo, hi):
+    """motionParaMeasure.m:22-33 / :49-60: center + (-e..e) moved to start at lo (when its
+    minimum is below lo) and to end at hi (when its maximum is above hi).  Both moves anchor
+    on a member of the set (find(==lo), find(==hi)); an empty find is a MATLAB error."""
+    cells = [center + k for k in range(-e, e + 1)]
+    if min(cells) < lo:
+        if lo not in cells:
+            raise IndexError("re-anchoring at the low edge: %d not in the cell set" % lo)
+        cells = [lo + k for k in range(2 * e + 1)]
+    if max(cells) > hi:
+        if hi not in cells:
+            raise IndexError("re-anchoring at the high edge: %d not in the cell set" % hi)
+        cells = [hi - k for k in range(2 * e + 1)]
+    return sorted(cells)
+
+
+def refine(values, cells, interp):
+    """interp1 spline over the cells + first max (:36-42 / :63-69): the 1-based cell of the
+    maximum (rCellMax / vCellMax)."""
+    y = np.asarray(values, dtype=np.float64)
+    m = spline_m(y)
+    q = colon(float(cells[0]), 1.0 / interp, float(cells[-1]))
+    best, bi = -np.inf, 0
+    for i, qi in enumerate(q):
+        v = spline_eval(y, m, qi - cells[0])
+        if v > best:
+            best, bi = v, i
+    return q[bi]
+
+
+def motion_para_measure(sum_rdm, diff_rdm, flag, extra_dots, r_scale, delta_r, r_interp,
+                        v_scale, delta_v, v_interp, k_value, beam_pos_num, beam_angle_step,
+                        ele_comp, ele_sys_err, mtd0_num, on_error="raise"):
+    """motionParaMeasure.m:1-88 on V x R arrays (MATLAB's echo_MTD_sum_short etc.);
+    k_value = kValues(freInd+1, beamPosNum+1).  Returns (rEst, vEst, eleEst, cells) with
+    cells[i] = (v, r), 0-based, of hit i.  on_error="nan" gives a hit the reference stops at
+    NaN estimates instead of raising (the batched device form's convention)."""
+    V, R = flag.shape
+    e = int(extra_dots)
+    hits = [(v, r) for r in range(R) for v in range(V) if flag[v, r]]       # find(), :6
+    r_est, v_est, ele = [], [], []
+    for v0, r0 in hits:
+        try:
+            re, ve, el = _measure_one(sum_rdm, diff_rdm, V, R, v0, r0, e, r_scale, delta_r, r_interp, v_scale,
+                                      delta_v, v_interp, k_value, beam_pos_num, beam_angle_step, ele_comp,
+                                      ele_sys_err, mtd0_num)
+        except IndexError:
+            if on_error != "nan":
+                raise
+            re = ve = el = float("nan")
+        r_est.append(re)
+        v_est.append(ve)
+        ele.append(el)
+    return np.array(r_est), np.array(v_est), np.array(ele), np.array(hits, dtype=np.int64).reshape(-1, 2)
+
+
+def _measure_one(sum_rdm, diff_rdm, V, R, v0, r0, e, r_scale, delta_r, r_interp, v_scale, delta_v, v_interp,
+                 k_value, beam_pos_num, beam_angle_step, ele_comp, ele_sys_err, mtd0_num):
+    """One hit of motionParaMeasure.m:17-86 (0-based cell v0, r0)."""
+    v1, r1 = v0 + 1, r0 + 1                                             # 1-based
+    rc = fix_cells(r1, e, 1, R)                                         # :22-33
+    if rc[0] < 1 or rc[-1] > R:
+        raise IndexError("range cells outside 1..%d" % R)
+    r_max = refine([sum_rdm[v0, c - 1] for c in rc], rc, r_interp)
+    re = float(r_scale[r0]) + (r_max - r1) * delta_r                    # :43
+    vc = fix_cells(v1, e, mtd0_num + 2, V - mtd0_num)                   # :49-60
+    if vc[0] < 1 or vc[-1] > V:
+        raise IndexError("velocity cells outside 1..%d" % V)
+    v_max = refine([sum_rdm[c - 1, r0] for c in vc], vc, v_interp)
+    fv = math.trunc(v_max)
+    ve = float(v_scale[fv - 1]) - (v_max - fv) * delta_v                # :70
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = np.float64(diff_rdm[v0, r0]) / np.float64(sum_rdm[v0, r0])   # :78
+    el = beam_pos_num * beam_angle_step + 2.5 - ratio * k_value + ele_comp + ele_sys_err   # :79
+    return re, ve, float(el)

@@ -1054,6 +1054,47 @@ int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t
     return RSP_OK;
 }
 
+// ------------------------------------------------------------------ post-detection measurement
+int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff, const uint8_t* d_flag, int64_t V,
+                           int64_t R, int64_t batch, const rsp_measure_params* mp, const double* d_r_scale,
+                           const double* d_v_scale, int64_t max_hits, double* d_est, int32_t* d_cells,
+                           int32_t* d_count, void* stream) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_motion_measure_dev: null ctx");
+    if (!mp || !d_sum || !d_diff || !d_flag || !d_r_scale || !d_v_scale || !d_count || batch < 0 || max_hits < 0 ||
+        (max_hits > 0 && !d_est))
+        return fail(ctx, RSP_ERR_ARG, "rsp_motion_measure_dev: bad argument");
+    const int64_t n = 2 * (int64_t)mp->extra_dots + 1;
+    if (mp->extra_dots < 1 || mp->extra_dots > 4)
+        return fail(ctx, RSP_ERR_UNSUPPORTED, "rsp_motion_measure_dev: extra_dots %d outside 1..4", mp->extra_dots);
+    if (mp->r_interp < 1 || mp->r_interp > 64 || mp->v_interp < 1 || mp->v_interp > 64)
+        return fail(ctx, RSP_ERR_ARG, "rsp_motion_measure_dev: interpolation factors %d, %d outside 1..64",
+                    mp->r_interp, mp->v_interp);
+    if (V < 1 || R < 1 || V > (1 << 20) || R > (1 << 20) || V * R > (int64_t)1 << 31 || batch > 0x7fffffff)
+        return fail(ctx, RSP_ERR_ARG, "rsp_motion_measure_dev: bad shape %lld x %lld x %lld", (long long)batch,
+                    (long long)V, (long long)R);
+    if (R < n || mp->mtd0_num < 0 || V - 2 * (int64_t)mp->mtd0_num - 1 < n)
+        return fail(ctx, RSP_ERR_ARG,
+                    "rsp_motion_measure_dev: %lld range bins / %lld unzeroed rows are fewer than 2*extraDots+1",
+                    (long long)R, (long long)(V - 2 * (int64_t)mp->mtd0_num - 1));
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    rsp::MeasureArgs a;
+    a.extra_dots = mp->extra_dots;
+    a.r_interp = mp->r_interp;
+    a.v_interp = mp->v_interp;
+    a.mtd0_num = mp->mtd0_num;
+    a.beam_pos_num = mp->beam_pos_num;
+    a.delta_r = mp->delta_r;
+    a.delta_v = mp->delta_v;
+    a.k_value = mp->k_value;
+    a.beam_angle_step = mp->beam_angle_step;
+    a.ele_comp = mp->ele_comp;
+    a.ele_sys_err = mp->ele_sys_err;
+    HIP_TRY(ctx, rsp::launch_measure(d_sum, d_diff, d_flag, (int)V, (int)R, (int)batch, a, d_r_scale, d_v_scale,
+                                     max_hits, d_est, d_cells, d_count, (hipStream_t)stream));
+    return RSP_OK;
+}
+
 // ------------------------------------------------------------------ raw-data ingest
 static int ingest_shape(rsp_ctx* ctx, const rsp_ingest_params* p, int64_t* rec) {
     if (!p) return fail(ctx, RSP_ERR_ARG, "ingest: null params");

@@ -117,6 +117,15 @@ struct MtdArgs {
 };
 
 // Raw-data ingest (rsp_ingest.hip): one frame of uniform DDC PRT records.
+// motionParaMeasure.m's scalar arguments (rsp_measure_params, rsp_measure.hip).
+struct MeasureArgs {
+    int extra_dots, r_interp, v_interp, mtd0_num, beam_pos_num;
+    double delta_r, delta_v, k_value, beam_angle_step, ele_comp, ele_sys_err;
+};
+hipError_t launch_measure(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
+                          const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
+                          double* est, int32_t* cells, int32_t* count, hipStream_t st);
+
 struct IngestArgs {
     int prt_num, point_prt, channel_num, beam_num;
     int bytes_head, bytes_realtime, bytes_tail;

@@ -30,7 +30,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check", "rsp_ingest_record_bytes",
-           "rsp_ingest_ddc_dev")
+           "rsp_ingest_ddc_dev", "rsp_motion_measure_dev")
 RSP_NKERNELS = 5
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "chain_kernel")
 
@@ -70,6 +70,13 @@ class rsp_ingest_params(C.Structure):
     _fields_ = [("prt_num", C.c_int32), ("point_prt", C.c_int32), ("channel_num", C.c_int32),
                 ("beam_num", C.c_int32), ("bytes_head", C.c_int32), ("bytes_realtime", C.c_int32),
                 ("bytes_tail", C.c_int32)]
+
+
+class rsp_measure_params(C.Structure):
+    _fields_ = [("extra_dots", C.c_int32), ("r_interp", C.c_int32), ("v_interp", C.c_int32),
+                ("mtd0_num", C.c_int32), ("beam_pos_num", C.c_int32), ("delta_r", C.c_double),
+                ("delta_v", C.c_double), ("k_value", C.c_double), ("beam_angle_step", C.c_double),
+                ("ele_comp", C.c_double), ("ele_sys_err", C.c_double)]
 
 
 # per-PRT ingest status codes (rsp_ingest_ddc_dev)
@@ -133,6 +140,9 @@ def load_library(path=None):
     lib.rsp_ingest_record_bytes.argtypes = [C.POINTER(rsp_ingest_params), C.POINTER(i64)]
     lib.rsp_ingest_ddc_dev.restype = C.c_int
     lib.rsp_ingest_ddc_dev.argtypes = [vp, vp, i64, C.POINTER(rsp_ingest_params), vp, vp, i64, vp, vp, vp]
+    lib.rsp_motion_measure_dev.restype = C.c_int
+    lib.rsp_motion_measure_dev.argtypes = [vp, vp, vp, vp, i64, i64, i64, C.POINTER(rsp_measure_params), vp, vp,
+                                           i64, vp, vp, vp, vp]
     lib.rsp_profile.restype = C.c_int
     lib.rsp_profile.argtypes = [vp, i32]
     lib.rsp_profile_read.restype = C.c_int
