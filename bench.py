@@ -37,6 +37,8 @@ CONFIGS = {
     "c5": dict(P=512, R=16384, batch=64, cfar=True, half=True, win=0),
     # SURVEY.md §8f-2 (not a BASELINE config): raw PRT records -> DBF beams, v2 capture frames
     "ingest": dict(P=332, R=3404, batch=8, cfar=False, half=False, win=0),
+    # motionParaMeasure over DMX long-part planes (2048 Doppler x 512 range)
+    "measure": dict(P=2048, R=512, batch=256, cfar=False, half=False, win=0),
 }
 
 
@@ -196,6 +198,110 @@ def bench_ingest(args, world, rank, local, dev, dist):
         dist.destroy_process_group()
 
 
+def bench_measure(args, world, rank, local, dev, dist):
+    """--config measure: CPIs/s through rsp_motion_measure_dev (motionParaMeasure.m:1-88) on
+    DMX long-part planes (V = 2048 Doppler rows x R = 512 range bins, the shape
+    DMX_SignalProcessing_main_xzr.m:489-494 measures), sum / diff / flag planes resident in
+    HBM; ~0.1 % of cells flagged (about 1000 hits per CPI), extraDots 2, interpolation 8 / 4
+    (the reference's :256-258 values).  Each rank measures its own CPIs (no collective)."""
+    import numpy as np
+    import torch
+    from rsp import measure, shard
+    B, V, R = args.batch, args.P, args.R
+    lo, _ = shard.weak_shard(B, rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4000 + lo)
+    s = torch.rand((B, V, R), generator=g, device=dev) * 2 + 0.1
+    d = torch.randn((B, V, R), generator=g, device=dev) * 0.5
+    M0 = 6
+    f = (torch.rand((B, V, R), generator=g, device=dev) < 1e-3).to(torch.uint8)
+    f[:, :M0 + 1, :] = 0                             # executeCFAR never flags the zeroed rows
+    f[:, V - M0:, :] = 0
+    meas = measure.Measure(local)
+    kv = measure.angle_KvalueGen(1)
+    p = meas.params(2, 5.996, 8, 0.2, 4, kv[4, 3], 3, 5.0, 0.0, 0.0, M0)
+    r_scale = np.arange(R) * 5.996
+    v_scale = -(np.arange(V) - V / 2) * 0.2
+    max_hits = 4096
+    stream = torch.cuda.current_stream(dev)
+    est, cells, count = meas.measure_dev(s, d, f, p, r_scale, v_scale, max_hits=max_hits)
+    torch.cuda.synchronize(dev)
+    hits = count[:, 0].double().mean().item()
+    assert int(count[:, 0].max()) <= max_hits and int(count[:, 1].sum()) == 0
+    rs = torch.as_tensor(r_scale, device=dev)
+    vs = torch.as_tensor(v_scale, device=dev)
+
+    import ctypes as C
+
+    def step():
+        rc = meas.lib.rsp_motion_measure_dev(meas.ctx, s.data_ptr(), d.data_ptr(), f.data_ptr(), V, R, B,
+                                             C.byref(p), rs.data_ptr(), vs.data_ptr(), max_hits, est.data_ptr(),
+                                             cells.data_ptr(), count.data_ptr(), C.c_void_p(stream.cuda_stream))
+        assert rc == 0
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import measure_ref
+        hs, hd, hf = s[0].double().cpu().numpy(), d[0].double().cpu().numpy(), f[0].cpu().numpy()
+        done, nh, t1 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds or done == 0:
+            re, _, _, _ = measure_ref.motion_para_measure(hs, hd, hf, 2, r_scale, 5.996, 8, v_scale, 0.2, 4,
+                                                          kv[4, 3], 3, 5.0, 0.0, 0.0, M0)
+            done += 1
+            nh += len(re)
+        el = time.perf_counter() - t1
+        cpu = {"value": done / el, "unit": "CPI/s", "cores": 1, "kind": "port",
+               "sample": "%d CPI(s) (%d hits) in %.1f s: fp64 Python restatement of motionParaMeasure.m, "
+                         "one thread" % (done, nh, el)}
+    if rank == 0:
+        # compulsory bytes per CPI: the flag plane, per hit 2 x (2e+1) sum cells + sum/diff at the
+        # hit + rScale/vScale entries read, 3 estimates + 2 cells written
+        unit_bytes = V * R + hits * (2 * 5 * 4 + 8 + 16 + 24 + 8)
+        per_cpi_s = gpu_ms / 1e3 / (args.steps * B)
+        ach = unit_bytes / per_cpi_s / 1e9
+        print(json.dumps({
+            "metric": "CPIs/sec (2048 Doppler x 512 range DMX long part, ~0.1% cells flagged) through "
+                      "motionParaMeasure (range/velocity spline refinement + elevation per CFAR hit)",
+            "value": round(world * B * args.steps / elapsed, 1), "unit": "CPI/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 in, f64",
+            "data": "synthetic planes (uniform sum, normal diff, Bernoulli(1e-3) flags, torch.Generator seeded)",
+            "config": {"workload": "measure: %d CPIs per GPU per step, planes resident in HBM" % B,
+                       "doppler": V, "range": R, "hits_per_cpi": round(hits, 1), "extra_dots": 2,
+                       "parallelism": "CPI-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "kernel": "hits_kernel + measure_kernel", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": None, "alg_bytes_per_unit": round(unit_bytes),
+                         "avg_launch_us": round(gpu_ms * 1e3 / args.steps, 2),
+                         "note": "one hits_kernel + one measure_kernel launch per step cover the whole batch; events around both"},
+            "cpu_baseline": cpu}), flush=True)
+    meas.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     args.warmup = max(args.warmup, 1)
@@ -214,6 +320,8 @@ def main():
     dev = torch.device("cuda", local)
     if args.config == "ingest":
         return bench_ingest(args, world, rank, local, dev, dist)
+    if args.config == "measure":
+        return bench_measure(args, world, rank, local, dev, dist)
 
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)

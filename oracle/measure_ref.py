@@ -80,12 +80,16 @@ def spline_m(y):
 
 
 def spline_eval(y, m, t):
-    """Value of the spline (y, m) at t in [0, n-1]; interval j = floor(t) clamped to n-2."""
+    """Value of the spline (y, m) at t in [0, n-1]: interval j = floor(t) clamped to n-2, in
+    Horner form y_j + u*(b_j + u*(c_j + u*d_j)) with u = t - j (the local power form MATLAB's
+    ppval evaluates)."""
     n = len(y)
     j = min(max(int(math.floor(t)), 0), n - 2)
     u = t - j
-    w = 1.0 - u
-    return w * y[j] + u * y[j + 1] + ((w * w * w - w) * m[j] + (u * u * u - u) * m[j + 1]) / 6.0
+    b = (y[j + 1] - y[j]) - (2.0 * m[j] + m[j + 1]) / 6.0
+    c = m[j] / 2.0
+    d = (m[j + 1] - m[j]) / 6.0
+    return y[j] + u * (b + u * (c + u * d))
 
 
 def fix_cells(center, e, lo, hi):

@@ -3,19 +3,25 @@
 // CFAR_WangCai/motionParaMeasure.m:1-88, called at DMX_SignalProcessing_main_xzr.m:489-494)
 // over a batch of CFAR flag matrices.
 //
-// One workgroup of 1024 threads per CPI, two passes over the [V][R] flag bytes:
-//   count  thread (slice s, column group g) counts the hits of its CW columns in its slice of
-//          rows; the counts are laid out in LDS in MATLAB's find() order (column, then row
-//          slice) and block-scanned there, which gives every (column, slice) its first output
-//          slot without sorting anything;
-//   emit   a thread re-reads only the columns it found hits in and measures each hit where it
-//          finds it: the 2e+1 cells around it re-anchored as the reference does, a not-a-knot
-//          cubic spline through their sum-channel values, its first maximum on the
-//          1/interp grid, and the amplitude-ratio elevation.
+// Two launches:
+//   hits_kernel     one workgroup of 1024 threads per CPI, two passes over the [V][R] flag
+//                   bytes.  count: thread (slice s, column group g) counts the hits of its CW
+//                   columns in its slice of rows; the counts are laid out in LDS in MATLAB's
+//                   find() order (column, then row slice) and block-scanned there, which gives
+//                   every (column, slice) its first output slot without sorting anything.
+//                   The count pass also keeps a 64-bit mask of which of the thread's row
+//                   groups hold hits; list: a thread re-reads only those rows and writes each
+//                   hit's cell index into its slot.
+//   measure_kernel  one thread per listed hit over the whole batch: the 2e+1 cells around it
+//                   re-anchored as the reference does, a not-a-knot cubic spline through their
+//                   sum-channel values, its first maximum on the 1/interp grid, and the
+//                   amplitude-ratio elevation.  Spreading hits over the chip (instead of
+//                   measuring them inside the CPI's workgroup) keeps the per-hit dependent
+//                   loads and fp64 work off the flag scan's critical path.
 // The measurement is fp64 with contraction off, in the same operation order as the oracle
-// (oracle/measure_ref.py), so the estimates are expected to be bit-identical to it.  The flag
-// pass is the HBM traffic (V*R bytes per CPI, read once from HBM, once more from cache for
-// the hit columns); the spline work is a few thousand fp64 operations per hit.
+// (oracle/measure_ref.py), so the estimates are bit-identical to it.  The flag scan is the
+// HBM traffic (V*R bytes per CPI, read once from HBM, once more from cache for the rows with
+// hits); the spline work is a few thousand fp64 operations per hit.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -76,35 +82,41 @@ __device__ __forceinline__ void spline_m(const double (&y)[N], double (&m)[N]) {
 }
 
 // The 1-based cell of the first maximum of the spline through y on cells first..first+N-1,
-// sampled at first : 1/interp : first+N-1 (motionParaMeasure.m:36-42, :63-69).
+// sampled at first : 1/interp : first+N-1 (motionParaMeasure.m:36-42, :63-69).  Each interval
+// j is evaluated in Horner form y_j + u*(b_j + u*(c_j + u*d_j)) (oracle/measure_ref.py
+// spline_eval); the samples are walked interval by interval (their abscissae are increasing),
+// so every coefficient stays in a register.
 template <int N>
 __device__ double refine(const double (&y)[N], int first, int interp) {
 #pragma clang fp contract(off)
     double m[N];
     spline_m<N>(y, m);
+    double cb[N - 1], cc[N - 1], cd[N - 1];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+        cb[j] = (y[j + 1] - y[j]) - (2.0 * m[j] + m[j + 1]) / 6.0;
+        cc[j] = m[j] / 2.0;
+        cd[j] = (m[j + 1] - m[j]) / 6.0;
+    }
     const double a = (double)first, b = (double)(first + N - 1);
     const double d = 1.0 / (double)interp;
     const int n = (int)floor((b - a) / d + 1e-10) + 1;
     double best = -INFINITY, qbest = a;
-    for (int i = 0; i < n; ++i) {
-        const double q = colon_at(a, d, b, i, n);
-        const double t = q - a;
-        int j = (int)floor(t);
-        j = j < 0 ? 0 : (j > N - 2 ? N - 2 : j);
-        const double u = t - (double)j, w = 1.0 - u;
-        double y0 = y[0], y1 = y[1], m0 = m[0], m1 = m[1];
+    int i = 0;
 #pragma unroll
-        for (int k = 1; k < N - 1; ++k)   // register select: no dynamic indexing
-            if (j == k) {
-                y0 = y[k];
-                y1 = y[k + 1];
-                m0 = m[k];
-                m1 = m[k + 1];
+    for (int j = 0; j < N - 1; ++j) {
+        for (; i < n; ++i) {
+            const double q = colon_at(a, d, b, i, n);
+            const double t = q - a;
+            int jj = (int)floor(t);
+            jj = jj < 0 ? 0 : (jj > N - 2 ? N - 2 : jj);
+            if (jj > j) break;
+            const double u = t - (double)j;
+            const double v = y[j] + u * (cb[j] + u * (cc[j] + u * cd[j]));
+            if (v > best) {
+                best = v;
+                qbest = q;
             }
-        const double v = w * y0 + u * y1 + ((w * w * w - w) * m0 + (u * u * u - u) * m1) / 6.0;
-        if (v > best) {
-            best = v;
-            qbest = q;
         }
     }
     return qbest;
@@ -141,17 +153,34 @@ __device__ void measure_hit(const float* __restrict__ sum, const float* __restri
         *bad = true;
         return;
     }
+    // every load up front (one round of latency): the range and velocity cells, the hit's
+    // sum / diff, rScale(r) and the N vScale entries fix(vCellMax) can select
+    float fr[N], fvv[N];
+    double vs[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        fr[k] = sum[(size_t)v0 * R + (rf - 1 + k)];
+        fvv[k] = sum[(size_t)(vf - 1 + k) * R + r0];
+        vs[k] = v_scale[vf - 1 + k];
+    }
+    const float s_hit = sum[(size_t)v0 * R + r0], d_hit = diff[(size_t)v0 * R + r0];
+    const double rs = r_scale[r0];
     double y[N];
 #pragma unroll
-    for (int k = 0; k < N; ++k) y[k] = (double)sum[(size_t)v0 * R + (rf - 1 + k)];
+    for (int k = 0; k < N; ++k) y[k] = (double)fr[k];
     const double r_max = refine<N>(y, rf, a.r_interp);
 #pragma unroll
-    for (int k = 0; k < N; ++k) y[k] = (double)sum[(size_t)(vf - 1 + k) * R + r0];
+    for (int k = 0; k < N; ++k) y[k] = (double)fvv[k];
     const double v_max = refine<N>(y, vf, a.v_interp);
     const double fv = trunc(v_max);
-    est[0] = r_scale[r0] + (r_max - (double)r1) * a.delta_r;                        // :43
-    est[1] = v_scale[(int)fv - 1] - (v_max - fv) * a.delta_v;                      // :70
-    const double ratio = (double)diff[(size_t)v0 * R + r0] / (double)sum[(size_t)v0 * R + r0];   // :78
+    const int kv = (int)fv - vf;   // 0..N-1: v_max lies in [vf, vf+N-1]
+    double vsel = vs[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+        if (kv == k) vsel = vs[k];
+    est[0] = rs + (r_max - (double)r1) * a.delta_r;                                  // :43
+    est[1] = vsel - (v_max - fv) * a.delta_v;                                        // :70
+    const double ratio = (double)d_hit / (double)s_hit;                              // :78
     est[2] = (double)a.beam_pos_num * a.beam_angle_step + 2.5 - ratio * a.k_value + a.ele_comp + a.ele_sys_err;   // :79
     *bad = false;
 }
@@ -186,29 +215,43 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int* total) {
     return r;
 }
 
-// CW columns per thread (4: one 32-bit load per row when R % 4 == 0), G column groups and
-// S = 1024 / G row slices per pass.
+// Bit j set where flag byte j of the CW at fl[v*R + c0] is nonzero (CW = 16: one 16-byte load).
+template <int CW>
+__device__ __forceinline__ uint32_t row_pattern(const uint8_t* __restrict__ fl, size_t off) {
+    if constexpr (CW == 16) {
+        const uint4 w = *reinterpret_cast<const uint4*>(fl + off);
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        uint32_t pat = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // high bit of each byte = byte nonzero
+            const uint32_t t = (((ws[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | ws[k]) & 0x80808080u;
+            pat |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * k);
+        }
+        return pat;
+    } else {
+        return fl[off] ? 1u : 0u;
+    }
+}
+
+// CW columns per thread (16: one 16-byte load per row when R % 16 == 0), G column groups and
+// S = 1024 / G row slices per pass; each thread owns `rows` rows of its CW columns.
 template <int E, int CW>
-__global__ __launch_bounds__(kThreads) void measure_kernel(const float* __restrict__ sum, const float* __restrict__ diff,
-                                                           const uint8_t* __restrict__ flag, int V, int R, int G,
-                                                           MeasureArgs a, const double* __restrict__ r_scale,
-                                                           const double* __restrict__ v_scale, int64_t max_hits,
-                                                           double* __restrict__ est, int32_t* __restrict__ cells,
-                                                           int32_t* __restrict__ count) {
+__global__ __launch_bounds__(kThreads) void hits_kernel(const uint8_t* __restrict__ flag, int V, int R, int G,
+                                                        int mtd0_num, int64_t max_hits, double* __restrict__ est,
+                                                        int32_t* __restrict__ count) {
     __shared__ int s_cnt[kThreads * CW];
     __shared__ int s_wave[33];
     __shared__ int s_bad;
     const int cpi = blockIdx.x;
     const size_t plane = (size_t)V * R;
     const uint8_t* fl = flag + cpi * plane;
-    const float* su = sum + cpi * plane;
-    const float* di = diff + cpi * plane;
-    double* es = est + (size_t)cpi * max_hits * 3;
-    int32_t* ce = cells ? cells + (size_t)cpi * max_hits * 2 : nullptr;
+    int64_t* hl = reinterpret_cast<int64_t*>(est) + (size_t)cpi * max_hits * 3;   // hit list, slot * 3
     const int S = kThreads / G;
     const int g = threadIdx.x % G, s = threadIdx.x / G;
     const int rows = (V + S - 1) / S;
-    const int v_lo = s * rows, v_hi = min(V, v_lo + rows);
+    const int v_lo = min(V, s * rows), v_hi = min(V, v_lo + rows);
+    const int q = (rows + 63) / 64;   // rows per bit of the thread's row mask
     if (threadIdx.x == 0) s_bad = 0;
     int base = 0;   // hits of the earlier column passes
     for (int c_pass = 0; c_pass < R; c_pass += G * CW) {
@@ -216,31 +259,28 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(const float* __restri
         int cnt[CW];
 #pragma unroll
         for (int j = 0; j < CW; ++j) cnt[j] = 0;
+        uint64_t rmask = 0;   // bit i: rows v_lo + i*q .. + q-1 hold a hit
         if (c0 < R) {
-            if constexpr (CW == 4) {
 #pragma unroll 8
-                for (int v = v_lo; v < v_hi; ++v) {
-                    const uint32_t w = *reinterpret_cast<const uint32_t*>(fl + (size_t)v * R + c0);
+            for (int v = v_lo; v < v_hi; ++v) {
+                const uint32_t pat = row_pattern<CW>(fl, (size_t)v * R + c0);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) cnt[j] += (w >> (8 * j)) & 0xffu ? 1 : 0;
-                }
-            } else {
-#pragma unroll 8
-                for (int v = v_lo; v < v_hi; ++v) cnt[0] += fl[(size_t)v * R + c0] ? 1 : 0;
+                for (int j = 0; j < CW; ++j) cnt[j] += (pat >> j) & 1u;
+                rmask |= (uint64_t)(pat != 0) << ((v - v_lo) / q);
             }
         }
         // counts in find() order: column c_pass + k (k = g*CW + j), then row slice s
 #pragma unroll
         for (int j = 0; j < CW; ++j) s_cnt[(g * CW + j) * S + s] = cnt[j];
         __syncthreads();
-        int run[CW], mine = 0;
+        int run[CW], part = 0;
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
             run[j] = s_cnt[threadIdx.x * CW + j];
-            mine += run[j];
+            part += run[j];
         }
         int total;
-        int pre = block_scan(mine, s_wave, &total);
+        int pre = block_scan(part, s_wave, &total);
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
             const int x = run[j];
@@ -248,34 +288,31 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(const float* __restri
             pre += x;
         }
         __syncthreads();
-        // emit: re-read the columns with hits, measure each hit in its slot
-#pragma unroll
-        for (int j = 0; j < CW; ++j) {
-            if (cnt[j] == 0) continue;
-            const int c = c0 + j;
-            int slot = s_cnt[(g * CW + j) * S + s];
-            int left = cnt[j];
-            for (int v = v_lo; v < v_hi && left > 0; ++v) {
-                if (!fl[(size_t)v * R + c]) continue;
-                --left;
-                if (slot < max_hits) {
-                    double e3[3];
-                    bool bad;
-                    measure_hit<E>(su, di, V, R, v, c, a, r_scale, v_scale, e3, &bad);
-                    es[(size_t)slot * 3 + 0] = e3[0];
-                    es[(size_t)slot * 3 + 1] = e3[1];
-                    es[(size_t)slot * 3 + 2] = e3[2];
-                    if (ce) {
-                        ce[(size_t)slot * 2 + 0] = v;
-                        ce[(size_t)slot * 2 + 1] = c;
+        // list: re-read only the row groups the mask marks (ascending rows), and give each hit
+        // its column's next slot; each (column, slice) keeps its next slot in its own LDS word,
+        // so the order is find()'s.
+        while (rmask) {
+            const int i = __builtin_ctzll(rmask);
+            rmask &= rmask - 1;
+            const int r_hi = min(v_hi, v_lo + (i + 1) * q);
+            for (int v = v_lo + i * q; v < r_hi; ++v) {
+                uint32_t pat = row_pattern<CW>(fl, (size_t)v * R + c0);
+                while (pat) {
+                    const int j = __builtin_ctz(pat);
+                    pat &= pat - 1;
+                    const int c = c0 + j;
+                    int* nx = &s_cnt[(g * CW + j) * S + s];
+                    const int slot = *nx;
+                    *nx = slot + 1;
+                    if (slot < max_hits) {
+                        hl[(size_t)slot * 3] = (int64_t)v * R + c;   // measured by measure_kernel
+                    } else {   // counted, not written: only whether the reference would stop here
+                        int f0;
+                        if (!fix_cells(c + 1, E, 1, R, R, &f0) ||
+                            !fix_cells(v + 1, E, mtd0_num + 2, V - mtd0_num, V, &f0))
+                            atomicAdd(&s_bad, 1);
                     }
-                    if (bad) atomicAdd(&s_bad, 1);
-                } else {   // counted, not written: only whether the reference would stop here
-                    int f0;
-                    if (!fix_cells(c + 1, E, 1, R, R, &f0) || !fix_cells(v + 1, E, a.mtd0_num + 2, V - a.mtd0_num, V, &f0))
-                        atomicAdd(&s_bad, 1);
                 }
-                ++slot;
             }
         }
         base += total;
@@ -283,24 +320,63 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(const float* __restri
     }
     if (threadIdx.x == 0) {
         count[cpi * 2 + 0] = base;
-        count[cpi * 2 + 1] = s_bad;
+        count[cpi * 2 + 1] = s_bad;   // measure_kernel adds the written hits' failures
     }
+}
+
+// One thread per listed hit (nb blocks per CPI): the cell index hits_kernel left in the first
+// word of the slot is replaced by the slot's three estimates.
+template <int E>
+__global__ __launch_bounds__(256) void measure_kernel(const float* __restrict__ sum, const float* __restrict__ diff,
+                                                      int V, int R, MeasureArgs a, const double* __restrict__ r_scale,
+                                                      const double* __restrict__ v_scale, int64_t max_hits,
+                                                      double* __restrict__ est, int32_t* __restrict__ cells,
+                                                      int32_t* __restrict__ count, unsigned nb) {
+    const int cpi = blockIdx.x / nb;
+    const int64_t slot = (int64_t)(blockIdx.x - (unsigned)cpi * nb) * 256 + threadIdx.x;
+    const int64_t n = count[cpi * 2];
+    if (slot >= n || slot >= max_hits) return;
+    const size_t plane = (size_t)V * R;
+    double* e = est + ((size_t)cpi * max_hits + slot) * 3;
+    const int64_t idx = *reinterpret_cast<const int64_t*>(e);
+    const int v = (int)(idx / R), c = (int)(idx - (int64_t)v * R);
+    double e3[3];
+    bool bad;
+    measure_hit<E>(sum + cpi * plane, diff + cpi * plane, V, R, v, c, a, r_scale, v_scale, e3, &bad);
+    e[0] = e3[0];
+    e[1] = e3[1];
+    e[2] = e3[2];
+    if (cells) {
+        cells[((size_t)cpi * max_hits + slot) * 2 + 0] = v;
+        cells[((size_t)cpi * max_hits + slot) * 2 + 1] = c;
+    }
+    if (bad) atomicAdd(&count[cpi * 2 + 1], 1);
 }
 
 template <int E>
 hipError_t launch_e(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
                     const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
                     double* est, int32_t* cells, int32_t* count, hipStream_t st) {
-    const bool wide = R % 4 == 0 && R >= 4 * 64 && ((uintptr_t)flag & 3) == 0;
-    int G = 64;   // column groups per pass: a power of two covering the columns, at most 1024
-    const int groups = wide ? R / 4 : R;
+    const bool wide = R % 16 == 0 && R >= 16 * 16 && ((uintptr_t)flag & 15) == 0;
+    // column groups per pass: a power of two covering the columns (16-byte groups: at least 16,
+    // one 256-byte row segment per 16 lanes; bytes: at least 64), at most 1024
+    int G = wide ? 16 : 64;
+    const int groups = wide ? R / 16 : R;
     while (G < groups && G < kThreads) G <<= 1;
     if (wide)
-        hipLaunchKernelGGL((measure_kernel<E, 4>), dim3(batch), dim3(kThreads), 0, st, sum, diff, flag, V, R, G, a,
-                           r_scale, v_scale, max_hits, est, cells, count);
+        hipLaunchKernelGGL((hits_kernel<E, 16>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.mtd0_num,
+                           max_hits, est, count);
     else
-        hipLaunchKernelGGL((measure_kernel<E, 1>), dim3(batch), dim3(kThreads), 0, st, sum, diff, flag, V, R, G, a,
-                           r_scale, v_scale, max_hits, est, cells, count);
+        hipLaunchKernelGGL((hits_kernel<E, 1>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.mtd0_num,
+                           max_hits, est, count);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess || max_hits == 0) return err;
+    // slots past a CPI's hit count exit at once; the grid covers max_hits (capped by V*R)
+    const int64_t cap = max_hits < (int64_t)V * R ? max_hits : (int64_t)V * R;
+    const int64_t nb = (cap + 255) / 256, blocks = nb * batch;   // blocks per CPI, total (1-D grid)
+    if (blocks > 0x7fffffff) return hipErrorInvalidConfiguration;
+    hipLaunchKernelGGL((measure_kernel<E>), dim3((unsigned)blocks), dim3(256), 0, st, sum, diff, V, R, a, r_scale,
+                       v_scale, max_hits, est, cells, count, (unsigned)nb);
     return hipGetLastError();
 }
 
