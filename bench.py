@@ -39,6 +39,8 @@ CONFIGS = {
     "ingest": dict(P=332, R=3404, batch=8, cfar=False, half=False, win=0),
     # motionParaMeasure over DMX long-part planes (2048 Doppler x 512 range)
     "measure": dict(P=2048, R=512, batch=256, cfar=False, half=False, win=0),
+    # iSTC gain + MTI (lag 30) on c3-shaped echoes ahead of the chain
+    "prefilter": dict(P=128, R=4096, batch=1024, cfar=False, half=False, win=0),
 }
 
 
@@ -198,6 +200,94 @@ def bench_ingest(args, world, rank, local, dev, dist):
         dist.destroy_process_group()
 
 
+def _timed(args, world, dev, dist, stream, step):
+    """W warmup steps, then K timed steps between barrier + synchronize; (wall s, event ms)."""
+    import torch
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1)
+
+
+def bench_prefilter(args, world, rank, local, dev, dist):
+    """--config prefilter: CPIs/s through rsp_prefilter_dev (fun_iSTC.m gain + fun_Process_MTI.m
+    lag-30 difference in one pass) on c3-shaped echoes (128 x 4096 complex64, 1024 CPIs per GPU),
+    resident in HBM; each rank filters its own CPIs (no collective)."""
+    import numpy as np
+    import torch
+    from rsp import prefilter, shard
+    B, P, R = args.batch, args.P, args.R
+    lo, _ = shard.weak_shard(B, rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5000 + lo)
+    x = torch.randn((B, P, R), dtype=torch.complex64, generator=g, device=dev)
+    out = torch.empty_like(x)
+    pf = prefilter.Prefilter(local)
+    stc = np.linspace(-30.0, 0.0, 1025)
+    _, gain = prefilter.istc_gain(stc, R)
+    d_gain = torch.from_numpy(gain).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    import ctypes as C
+
+    def step():
+        rc = pf.lib.rsp_prefilter_dev(pf.ctx, x.data_ptr(), out.data_ptr(), P, R, B, d_gain.data_ptr(), 30,
+                                      C.c_void_p(stream.cuda_stream))
+        assert rc == 0
+
+    elapsed, gpu_ms = _timed(args, world, dev, dist, stream, step)
+    if world > 1:
+        elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import prefilter_ref
+        hx = x[:4].cpu().numpy().astype(np.complex128)
+        done, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds or done == 0:
+            prefilter_ref.fun_iSTC(prefilter_ref.fun_Process_MTI(hx[done % 4]), stc)
+            done += 1
+        el = time.perf_counter() - t1
+        cpu = {"value": done / el, "unit": "CPI/s", "cores": 1, "kind": "port",
+               "sample": "%d CPIs in %.1f s: fp64 numpy restatement (row loops as fun_Process_MTI.m / "
+                         "fun_iSTC.m), one thread" % (done, el)}
+    if rank == 0:
+        unit_bytes = 2 * P * R * 8                                   # echo read once + written once
+        per_launch_s = gpu_ms / 1e3 / args.steps
+        ach = unit_bytes * B / per_launch_s / 1e9
+        print(json.dumps({
+            "metric": "CPIs/sec (4096 range x 128 pulse) through the echo pre-filters (iSTC gain + MTI lag 30)",
+            "value": round(world * B * args.steps / elapsed, 1), "unit": "CPI/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c64 (f32)",
+            "data": "synthetic echo (torch.randn complex64, seeded), 1025-point stc ramp",
+            "config": {"workload": "prefilter: %d CPIs per GPU per step, echo resident in HBM" % B,
+                       "pulses": P, "range": R, "mti_lag": 30,
+                       "parallelism": "CPI-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "kernel": "prefilter_kernel<true,true>", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": None, "alg_bytes_per_unit": unit_bytes,
+                         "avg_launch_us": round(per_launch_s * 1e6, 2),
+                         "note": "one launch per step over the whole batch; events around the launches"},
+            "cpu_baseline": cpu}), flush=True)
+    pf.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def bench_measure(args, world, rank, local, dev, dist):
     """--config measure: CPIs/s through rsp_motion_measure_dev (motionParaMeasure.m:1-88) on
     DMX long-part planes (V = 2048 Doppler rows x R = 512 range bins, the shape
@@ -322,6 +412,8 @@ def main():
         return bench_ingest(args, world, rank, local, dev, dist)
     if args.config == "measure":
         return bench_measure(args, world, rank, local, dev, dist)
+    if args.config == "prefilter":
+        return bench_prefilter(args, world, rank, local, dev, dist)
 
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)

@@ -316,6 +316,19 @@ int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff
                            const double* d_r_scale, const double* d_v_scale, int64_t max_hits,
                            double* d_est, int32_t* d_cells /* nullable */, int32_t* d_count, void* stream);
 
+/* ---- echo pre-filters ---------------------------------------------------- */
+/* iSTC and MTI on a device-resident echo batch, complex64 [batch][P][R] (row = pulse, the
+ * chain's ROWMAJOR layout), before pulse compression:
+ *   d_gain != NULL: out(m, n) *= d_gain[n], the linear gain 10^(stc(n)/20) of
+ *       [stc, eoch_iSTC] = fun_iSTC(echo)            (MTD/fun_iSTC.m:12-15; the caller reads
+ *       the stc curve and zero-pads it to R as :8-9 do -- rsp/prefilter.py istc_gain);
+ *   mti_lag > 0: out(m, :) = x(m+lag, :) - x(m, :) for m < P-lag, 0 for the last lag rows,
+ *       MTI_Out = fun_Process_MTI(ProSiganl)          (MTD/fun_Process_MTI.m:9,20-22; lag 30).
+ * Both: the MTI difference first, then the gain (the two commute up to fp32 rounding).
+ * R must be even and d_in / d_out 16-byte aligned; d_out == d_in is allowed only without MTI. */
+int rsp_prefilter_dev(rsp_ctx* ctx, const void* d_in, void* d_out, int64_t P, int64_t R, int64_t batch,
+                      const float* d_gain /* nullable, [R] */, int32_t mti_lag, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1

@@ -1095,6 +1095,25 @@ int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff
     return RSP_OK;
 }
 
+// ------------------------------------------------------------------ echo pre-filters
+int rsp_prefilter_dev(rsp_ctx* ctx, const void* d_in, void* d_out, int64_t P, int64_t R, int64_t batch,
+                      const float* d_gain, int32_t mti_lag, void* stream) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_prefilter_dev: null ctx");
+    if (!d_in || !d_out || P < 1 || R < 2 || batch < 0 || mti_lag < 0)
+        return fail(ctx, RSP_ERR_ARG, "rsp_prefilter_dev: bad argument");
+    if (R % 2 != 0 || ((uintptr_t)d_in & 15) || ((uintptr_t)d_out & 15))
+        return fail(ctx, RSP_ERR_UNSUPPORTED, "rsp_prefilter_dev: needs an even R and 16-byte aligned buffers");
+    if (P > (1 << 24) || R > (1 << 24))
+        return fail(ctx, RSP_ERR_ARG, "rsp_prefilter_dev: bad shape %lld x %lld", (long long)P, (long long)R);
+    if (mti_lag > 0 && d_in == d_out)
+        return fail(ctx, RSP_ERR_ARG, "rsp_prefilter_dev: MTI cannot run in place");
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    HIP_TRY(ctx, rsp::launch_prefilter((const float2*)d_in, (float2*)d_out, d_gain, (int)P, (int)R, batch, mti_lag,
+                                       (hipStream_t)stream));
+    return RSP_OK;
+}
+
 // ------------------------------------------------------------------ raw-data ingest
 static int ingest_shape(rsp_ctx* ctx, const rsp_ingest_params* p, int64_t* rec) {
     if (!p) return fail(ctx, RSP_ERR_ARG, "ingest: null params");

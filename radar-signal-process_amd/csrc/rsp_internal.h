@@ -126,6 +126,10 @@ hipError_t launch_measure(const float* sum, const float* diff, const uint8_t* fl
                           const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
                           double* est, int32_t* cells, int32_t* count, hipStream_t st);
 
+// Echo pre-filters (rsp_prefilter.hip): iSTC gain per range bin and/or MTI row difference.
+hipError_t launch_prefilter(const float2* in, float2* out, const float* gain, int P, int R, int64_t batch, int lag,
+                            hipStream_t st);
+
 struct IngestArgs {
     int prt_num, point_prt, channel_num, beam_num;
     int bytes_head, bytes_realtime, bytes_tail;

@@ -30,7 +30,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check", "rsp_ingest_record_bytes",
-           "rsp_ingest_ddc_dev", "rsp_motion_measure_dev")
+           "rsp_ingest_ddc_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev")
 RSP_NKERNELS = 5
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "chain_kernel")
 
@@ -143,6 +143,8 @@ def load_library(path=None):
     lib.rsp_motion_measure_dev.restype = C.c_int
     lib.rsp_motion_measure_dev.argtypes = [vp, vp, vp, vp, i64, i64, i64, C.POINTER(rsp_measure_params), vp, vp,
                                            i64, vp, vp, vp, vp]
+    lib.rsp_prefilter_dev.restype = C.c_int
+    lib.rsp_prefilter_dev.argtypes = [vp, vp, vp, i64, i64, i64, vp, i32, vp]
     lib.rsp_profile.restype = C.c_int
     lib.rsp_profile.argtypes = [vp, i32]
     lib.rsp_profile_read.restype = C.c_int
