@@ -265,6 +265,8 @@ def bench_prefilter(args, world, rank, local, dev, dist):
                          "fun_iSTC.m), one thread" % (done, el)}
     if rank == 0:
         unit_bytes = 2 * P * R * 8                                   # echo read once + written once
+        pmc = pmc_traffic("prefilter")
+        traffic = pmc["kernels"].get("mti_chain_kernel", {}).get("hbm_bytes_per_launch") if pmc else None
         per_launch_s = gpu_ms / 1e3 / args.steps
         ach = unit_bytes * B / per_launch_s / 1e9
         print(json.dumps({
@@ -276,9 +278,9 @@ def bench_prefilter(args, world, rank, local, dev, dist):
             "config": {"workload": "prefilter: %d CPIs per GPU per step, echo resident in HBM" % B,
                        "pulses": P, "range": R, "mti_lag": 30,
                        "parallelism": "CPI-sharded x%d, no collective" % world},
-            "roofline": {"bound": "hbm", "kernel": "prefilter_kernel<true,true>", "achieved": round(ach, 1),
+            "roofline": {"bound": "hbm", "kernel": "mti_chain_kernel<true>", "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "traffic": None, "alg_bytes_per_unit": unit_bytes,
+                         "traffic": traffic, "traffic_source": "profiles/pmc_prefilter.json (bytes per launch)", "alg_bytes_per_unit": unit_bytes,
                          "avg_launch_us": round(per_launch_s * 1e6, 2),
                          "note": "one launch per step over the whole batch; events around the launches"},
             "cpu_baseline": cpu}), flush=True)
@@ -368,6 +370,9 @@ def bench_measure(args, world, rank, local, dev, dist):
         # compulsory bytes per CPI: the flag plane, per hit 2 x (2e+1) sum cells + sum/diff at the
         # hit + rScale/vScale entries read, 3 estimates + 2 cells written
         unit_bytes = V * R + hits * (2 * 5 * 4 + 8 + 16 + 24 + 8)
+        pmc = pmc_traffic("measure")
+        traffic = sum(pmc["kernels"].get(k, {}).get("hbm_bytes_per_launch", 0)
+                      for k in ("hits_kernel", "measure_kernel")) if pmc else None
         per_cpi_s = gpu_ms / 1e3 / (args.steps * B)
         ach = unit_bytes / per_cpi_s / 1e9
         print(json.dumps({
@@ -382,7 +387,7 @@ def bench_measure(args, world, rank, local, dev, dist):
                        "parallelism": "CPI-sharded x%d, no collective" % world},
             "roofline": {"bound": "hbm", "kernel": "hits_kernel + measure_kernel", "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "traffic": None, "alg_bytes_per_unit": round(unit_bytes),
+                         "traffic": traffic, "traffic_source": "profiles/pmc_measure.json (both launches of a step)", "alg_bytes_per_unit": round(unit_bytes),
                          "avg_launch_us": round(gpu_ms * 1e3 / args.steps, 2),
                          "note": "one hits_kernel + one measure_kernel launch per step cover the whole batch; events around both"},
             "cpu_baseline": cpu}), flush=True)

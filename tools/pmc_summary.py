@@ -19,7 +19,9 @@ LABELS = (("pc_persist_kernel", "pc_kernel"), ("pc_mf_kernel", "pc_kernel"), ("p
           ("mtd_bluestein_kernel", "mtd_kernel"), ("mtd_kernel", "mtd_kernel"),
           ("cfar_hits_kernel", "cfar_r_kernel"), ("cfar_r16_kernel", "cfar_r_kernel"),
           ("cfar_r_kernel", "cfar_r_kernel"), ("cfar_r_generic_kernel", "cfar_r_kernel"),
-          ("cfar_v_kernel", "cfar_v_kernel"), ("fillBuffer", "flag_memset"))
+          ("cfar_v_kernel", "cfar_v_kernel"), ("fillBuffer", "flag_memset"), ("hits_kernel", "hits_kernel"),
+          ("measure_kernel", "measure_kernel"), ("prefilter_kernel", "prefilter_kernel"), ("mti_chain_kernel", "mti_chain_kernel"),
+          ("ingest_ddc_kernel", "ingest_ddc_kernel"), ("ingest_check_kernel", "ingest_check_kernel"))
 
 
 def short(name):
@@ -47,7 +49,7 @@ def main():
     acc, dur = load(pmc_dir)
     rows = {}
     for k, cs in acc.items():
-        if not any(x in k for x in ("pc_", "mtd", "cfar", "memset")):
+        if not any(x in k for x in ("pc_", "mtd", "cfar", "memset", "hits_kernel", "measure_kernel", "prefilter_kernel", "mti_chain", "ingest")):
             continue
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         d = sum(dur[k]) / len(dur[k]) if dur[k] else float("nan")
