@@ -296,7 +296,8 @@ int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, co
  * d_cells != NULL, d_cells[(cpi*max_hits + i)*2 + {0,1}] = its 0-based (row, column).
  * d_count[cpi*2] = hits in the CPI (only the first max_hits are written), d_count[cpi*2+1] =
  * hits the reference stops at with an index error (a hit too close to an edge for the
- * re-anchoring at :24-32 / :51-59); their estimates are NaN. */
+ * re-anchoring at :24-32 / :51-59); their estimates are NaN.  With mp->ld > R the three
+ * planes are R-column windows of rows ld elements apart. */
 typedef struct {
     int32_t extra_dots;      /* extraDots (2), 1..4: 2*extraDots+1 cells per spline */
     int32_t r_interp;        /* rInterpTimes (8), 1..64 */
@@ -309,6 +310,11 @@ typedef struct {
     double beam_angle_step;  /* beamAngleStep [deg] (5) */
     double ele_comp;         /* eleAngleComp */
     double ele_sys_err;      /* eleAngleSysErr */
+    int64_t ld;              /* row pitch of the planes in elements (0 = R): a column window of a
+                                wider plane, e.g. DMX's short part (columns 0..61) or long part
+                                (62..573, pass the planes + 62) measured separately as the
+                                reference does (DMX_SignalProcessing_main_xzr.m:489-494) */
+    int64_t cpi_stride;      /* elements between CPIs (0 = V * ld) */
 } rsp_measure_params;
 
 int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff, const uint8_t* d_flag,

@@ -1076,9 +1076,15 @@ int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff
         return fail(ctx, RSP_ERR_ARG,
                     "rsp_motion_measure_dev: %lld range bins / %lld unzeroed rows are fewer than 2*extraDots+1",
                     (long long)R, (long long)(V - 2 * (int64_t)mp->mtd0_num - 1));
+    const int64_t ld = mp->ld ? mp->ld : R, cs = mp->cpi_stride ? mp->cpi_stride : V * ld;
+    if (ld < R || cs < (V - 1) * ld + R)
+        return fail(ctx, RSP_ERR_ARG, "rsp_motion_measure_dev: row pitch %lld / CPI stride %lld too small for %lld x %lld",
+                    (long long)ld, (long long)cs, (long long)V, (long long)R);
     if (batch == 0) return RSP_OK;
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
     rsp::MeasureArgs a;
+    a.ld = ld;
+    a.cs = cs;
     a.extra_dots = mp->extra_dots;
     a.r_interp = mp->r_interp;
     a.v_interp = mp->v_interp;

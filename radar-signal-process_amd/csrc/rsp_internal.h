@@ -121,6 +121,7 @@ struct MtdArgs {
 struct MeasureArgs {
     int extra_dots, r_interp, v_interp, mtd0_num, beam_pos_num;
     double delta_r, delta_v, k_value, beam_angle_step, ele_comp, ele_sys_err;
+    int64_t ld, cs;   // row pitch and CPI stride of the planes, in elements
 };
 hipError_t launch_measure(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
                           const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,

@@ -159,11 +159,11 @@ __device__ void measure_hit(const float* __restrict__ sum, const float* __restri
     double vs[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        fr[k] = sum[(size_t)v0 * R + (rf - 1 + k)];
-        fvv[k] = sum[(size_t)(vf - 1 + k) * R + r0];
+        fr[k] = sum[(size_t)v0 * a.ld + (rf - 1 + k)];
+        fvv[k] = sum[(size_t)(vf - 1 + k) * a.ld + r0];
         vs[k] = v_scale[vf - 1 + k];
     }
-    const float s_hit = sum[(size_t)v0 * R + r0], d_hit = diff[(size_t)v0 * R + r0];
+    const float s_hit = sum[(size_t)v0 * a.ld + r0], d_hit = diff[(size_t)v0 * a.ld + r0];
     const double rs = r_scale[r0];
     double y[N];
 #pragma unroll
@@ -238,14 +238,13 @@ __device__ __forceinline__ uint32_t row_pattern(const uint8_t* __restrict__ fl, 
 // S = 1024 / G row slices per pass; each thread owns `rows` rows of its CW columns.
 template <int E, int CW>
 __global__ __launch_bounds__(kThreads) void hits_kernel(const uint8_t* __restrict__ flag, int V, int R, int G,
-                                                        int mtd0_num, int64_t max_hits, double* __restrict__ est,
+                                                        int64_t ld, int64_t cs, int mtd0_num, int64_t max_hits, double* __restrict__ est,
                                                         int32_t* __restrict__ count) {
     __shared__ int s_cnt[kThreads * CW];
     __shared__ int s_wave[33];
     __shared__ int s_bad;
     const int cpi = blockIdx.x;
-    const size_t plane = (size_t)V * R;
-    const uint8_t* fl = flag + cpi * plane;
+    const uint8_t* fl = flag + cpi * cs;
     int64_t* hl = reinterpret_cast<int64_t*>(est) + (size_t)cpi * max_hits * 3;   // hit list, slot * 3
     const int S = kThreads / G;
     const int g = threadIdx.x % G, s = threadIdx.x / G;
@@ -263,7 +262,7 @@ __global__ __launch_bounds__(kThreads) void hits_kernel(const uint8_t* __restric
         if (c0 < R) {
 #pragma unroll 8
             for (int v = v_lo; v < v_hi; ++v) {
-                const uint32_t pat = row_pattern<CW>(fl, (size_t)v * R + c0);
+                const uint32_t pat = row_pattern<CW>(fl, (size_t)v * ld + c0);
 #pragma unroll
                 for (int j = 0; j < CW; ++j) cnt[j] += (pat >> j) & 1u;
                 rmask |= (uint64_t)(pat != 0) << ((v - v_lo) / q);
@@ -296,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void hits_kernel(const uint8_t* __restric
             rmask &= rmask - 1;
             const int r_hi = min(v_hi, v_lo + (i + 1) * q);
             for (int v = v_lo + i * q; v < r_hi; ++v) {
-                uint32_t pat = row_pattern<CW>(fl, (size_t)v * R + c0);
+                uint32_t pat = row_pattern<CW>(fl, (size_t)v * ld + c0);
                 while (pat) {
                     const int j = __builtin_ctz(pat);
                     pat &= pat - 1;
@@ -336,7 +335,7 @@ __global__ __launch_bounds__(256) void measure_kernel(const float* __restrict__ 
     const int64_t slot = (int64_t)(blockIdx.x - (unsigned)cpi * nb) * 256 + threadIdx.x;
     const int64_t n = count[cpi * 2];
     if (slot >= n || slot >= max_hits) return;
-    const size_t plane = (size_t)V * R;
+    const size_t plane = (size_t)a.cs;
     double* e = est + ((size_t)cpi * max_hits + slot) * 3;
     const int64_t idx = *reinterpret_cast<const int64_t*>(e);
     const int v = (int)(idx / R), c = (int)(idx - (int64_t)v * R);
@@ -357,17 +356,17 @@ template <int E>
 hipError_t launch_e(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
                     const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
                     double* est, int32_t* cells, int32_t* count, hipStream_t st) {
-    const bool wide = R % 16 == 0 && R >= 16 * 16 && ((uintptr_t)flag & 15) == 0;
+    const bool wide = R % 16 == 0 && R >= 16 * 16 && a.ld % 16 == 0 && a.cs % 16 == 0 && ((uintptr_t)flag & 15) == 0;
     // column groups per pass: a power of two covering the columns (16-byte groups: at least 16,
     // one 256-byte row segment per 16 lanes; bytes: at least 64), at most 1024
     int G = wide ? 16 : 64;
     const int groups = wide ? R / 16 : R;
     while (G < groups && G < kThreads) G <<= 1;
     if (wide)
-        hipLaunchKernelGGL((hits_kernel<E, 16>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.mtd0_num,
+        hipLaunchKernelGGL((hits_kernel<E, 16>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.ld, a.cs, a.mtd0_num,
                            max_hits, est, count);
     else
-        hipLaunchKernelGGL((hits_kernel<E, 1>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.mtd0_num,
+        hipLaunchKernelGGL((hits_kernel<E, 1>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.ld, a.cs, a.mtd0_num,
                            max_hits, est, count);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess || max_hits == 0) return err;

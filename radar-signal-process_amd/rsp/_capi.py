@@ -76,7 +76,8 @@ class rsp_measure_params(C.Structure):
     _fields_ = [("extra_dots", C.c_int32), ("r_interp", C.c_int32), ("v_interp", C.c_int32),
                 ("mtd0_num", C.c_int32), ("beam_pos_num", C.c_int32), ("delta_r", C.c_double),
                 ("delta_v", C.c_double), ("k_value", C.c_double), ("beam_angle_step", C.c_double),
-                ("ele_comp", C.c_double), ("ele_sys_err", C.c_double)]
+                ("ele_comp", C.c_double), ("ele_sys_err", C.c_double), ("ld", C.c_int64),
+                ("cpi_stride", C.c_int64)]
 
 
 # per-PRT ingest status codes (rsp_ingest_ddc_dev)

@@ -11,7 +11,8 @@ every CFAR hit, with the reference's names and argument meaning:
     device layout of rsp_pc_mtd_cfar_diff_dev's outputs); the series come back in MATLAB's
     find() order.  A hit the reference cannot re-anchor (it stops with an index error there)
     raises IndexError here too.
-  * Measure.measure_dev(...): the batched device form, [batch][V][R] in, per-CPI hit lists out.
+  * Measure.measure_dev(...): the batched device form, [batch][V][R] in (optionally a column
+    window of wider planes), per-CPI hit lists out.
   * angle_KvalueGen(sysNum), freValueGen(freInd): the calibration lookups of
     CFAR_WangCai/angle_KvalueGen.m and freValueGen.m.
 
@@ -97,22 +98,30 @@ class Measure:
             return x.to(self.device, dtype).contiguous()
         return torch.as_tensor(np.ascontiguousarray(x), device=self.device).to(dtype).contiguous()
 
-    def measure_dev(self, sum_rdm, diff_rdm, flag, params, r_scale, v_scale, max_hits=None, stream=None):
-        """Batched: sum_rdm / diff_rdm float32 [batch][V][R], flag uint8 [batch][V][R] (device
-        tensors, or arrays copied to the device).  Returns (est float64 [batch][max_hits][3],
-        cells int32 [batch][max_hits][2], count int32 [batch][2]) on the device; count[:, 0] is
-        the hit count of each CPI (hits past max_hits are counted, not written) and count[:, 1]
-        the hits the reference would stop at with an index error."""
+    def measure_dev(self, sum_rdm, diff_rdm, flag, params, r_scale, v_scale, max_hits=None, stream=None,
+                    cols=None):
+        """Batched: sum_rdm / diff_rdm float32 [batch][V][Rp], flag uint8 [batch][V][Rp] (device
+        tensors, or arrays copied to the device).  cols = (lo, hi) measures the column window
+        lo..hi-1 of every plane in place (e.g. DMX's short / long part), as the reference
+        measures each part's own matrices; default all columns.  Returns (est float64
+        [batch][max_hits][3], cells int32 [batch][max_hits][2] relative to the window, count
+        int32 [batch][2]) on the device; count[:, 0] is the hit count of each CPI (hits past
+        max_hits are counted, not written) and count[:, 1] the hits the reference would stop
+        at with an index error."""
         import torch
         s = self._dev(sum_rdm, torch.float32)
         d = self._dev(diff_rdm, torch.float32)
         f = self._dev(flag, torch.uint8)
         if s.dim() == 2:
             s, d, f = s[None], d[None], f[None]
-        B, V, R = s.shape
+        B, V, Rp = s.shape
         if d.shape != s.shape or f.shape != s.shape:
             raise ValueError("measure_dev: sum %s, diff %s and flag %s differ in shape"
                              % (tuple(s.shape), tuple(d.shape), tuple(f.shape)))
+        lo, hi = (0, Rp) if cols is None else (int(cols[0]), int(cols[1]))
+        if not 0 <= lo < hi <= Rp:
+            raise ValueError("measure_dev: column window %r outside 0..%d" % ((lo, hi), Rp))
+        R = hi - lo
         rs = self._dev(np.asarray(r_scale, dtype=np.float64).reshape(-1), torch.float64)
         vs = self._dev(np.asarray(v_scale, dtype=np.float64).reshape(-1), torch.float64)
         if rs.numel() < R or vs.numel() < V:
@@ -122,12 +131,27 @@ class Measure:
         est = torch.empty((B, max_hits, 3), dtype=torch.float64, device=self.device)
         cells = torch.empty((B, max_hits, 2), dtype=torch.int32, device=self.device)
         count = torch.empty((B, 2), dtype=torch.int32, device=self.device)
+        params.ld, params.cpi_stride = Rp, V * Rp
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         capi.check(self.lib.rsp_motion_measure_dev(
-            self.ctx, s.data_ptr(), d.data_ptr(), f.data_ptr(), V, R, B, C.byref(params), rs.data_ptr(),
-            vs.data_ptr(), max_hits, est.data_ptr(), cells.data_ptr(), count.data_ptr(), C.c_void_p(st)), self.ctx)
+            self.ctx, s.data_ptr() + 4 * lo, d.data_ptr() + 4 * lo, f.data_ptr() + lo, V, R, B, C.byref(params),
+            rs.data_ptr(), vs.data_ptr(), max_hits, est.data_ptr(), cells.data_ptr(), count.data_ptr(),
+            C.c_void_p(st)), self.ctx)
         self._keep = (s, d, f, rs, vs)    # alive until the caller synchronises
         return est, cells, count
+
+    @staticmethod
+    def series(est, count, bad_raises=True):
+        """Per-CPI (rEst, vEst, eleEst) numpy columns from measure_dev's outputs (synchronises)."""
+        e, n = est.cpu().numpy(), count.cpu().numpy()
+        out = []
+        for b in range(e.shape[0]):
+            if bad_raises and n[b, 1]:
+                raise IndexError("motionParaMeasure: %d hit(s) too close to an edge for the reference's "
+                                 "re-anchoring (motionParaMeasure.m:24-32, :51-59)" % n[b, 1])
+            k = min(int(n[b, 0]), e.shape[1])
+            out.append((e[b, :k, 0].copy(), e[b, :k, 1].copy(), e[b, :k, 2].copy()))
+        return out
 
     def motionParaMeasure(self, echo_MTD_sum, echo_MTD_diff, cfarResultFlag_Matrix, extraDots, rScale, deltaR,  # noqa: N802
                           rInterpTimes, vScale, deltaV, vInterpTimes, kValues, beamPosNum, beamAngleStep, freInd,

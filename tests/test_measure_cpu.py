@@ -128,3 +128,20 @@ def test_calibration_tables():
         freValueGen(11)
     with pytest.raises(ValueError):
         angle_KvalueGen(3)
+
+
+def test_dmx_scales():
+    """DMX_SignalProcessing_main_xzr.m:93-96, :250-253, :313-327: deltaR = c*ts/2, the range
+    calibration offsets, deltaV = lambda*prf/N/2, vScale = -lambda*fftshift(f)/2."""
+    from rsp import presets
+    from rsp.dmx import dmx_scales
+    from rsp.measure import freValueGen
+    spec = presets.dmx_native(fc=freValueGen(3))
+    rS, rL, vS, dR, dV = dmx_scales(spec, 3)
+    assert dR == pytest.approx(2.99792458e8 / 12.5e6 / 2)
+    assert rS.shape == (62,) and rS[0] == -297.0 and rS[1] - rS[0] == pytest.approx(dR)
+    assert rL.shape == (512,) and rL[0] == 62 * 12 - 92.0
+    lam = 2.99792458e8 / 9385e6
+    assert dV == pytest.approx(lam * (1 / 52.08e-6) / 2048 / 2)
+    assert vS.shape == (2048,) and vS[0] == 0 and vS[1] == pytest.approx(-dV) and vS[-1] == pytest.approx(dV)
+    assert vS[1024] == pytest.approx(1024 * dV)          # fftshift puts -N/2 at index N/2
