@@ -49,6 +49,7 @@ struct rsp_ctx {
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
+    DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
     bool fused = false;                 // one-launch chain where the shape has one (rsp_set_fused)
     DevBuf chain_ctl;                   // fused chain: queue heads, stage counters, timeout word
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
@@ -204,7 +205,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
-                      &ctx->chain_ctl};
+                      &ctx->chain_ctl, &ctx->meas_band};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -1096,8 +1097,14 @@ int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff
     a.beam_angle_step = mp->beam_angle_step;
     a.ele_comp = mp->ele_comp;
     a.ele_sys_err = mp->ele_sys_err;
+    const int nb = rsp::measure_bands((int)V, (int)batch);
+    if (nb > 1) {
+        const int rc = ensure(ctx, ctx->meas_band, (size_t)batch * nb * R * sizeof(int32_t));
+        if (rc != RSP_OK) return rc;
+    }
     HIP_TRY(ctx, rsp::launch_measure(d_sum, d_diff, d_flag, (int)V, (int)R, (int)batch, a, d_r_scale, d_v_scale,
-                                     max_hits, d_est, d_cells, d_count, (hipStream_t)stream));
+                                     max_hits, d_est, d_cells, d_count, (int32_t*)ctx->meas_band.p, nb,
+                                     (hipStream_t)stream));
     return RSP_OK;
 }
 

@@ -123,9 +123,12 @@ struct MeasureArgs {
     double delta_r, delta_v, k_value, beam_angle_step, ele_comp, ele_sys_err;
     int64_t ld, cs;   // row pitch and CPI stride of the planes, in elements
 };
+// Workgroups per CPI for the hit lists (1: hits_kernel; > 1: the banded path, which needs
+// batch * nb * R int32 of scratch in band_cnt).
+int measure_bands(int V, int batch);
 hipError_t launch_measure(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
                           const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
-                          double* est, int32_t* cells, int32_t* count, hipStream_t st);
+                          double* est, int32_t* cells, int32_t* count, int32_t* band_cnt, int nb, hipStream_t st);
 
 // Echo pre-filters (rsp_prefilter.hip): iSTC gain per range bin and/or MTI row difference.
 hipError_t launch_prefilter(const float2* in, float2* out, const float* gain, int P, int R, int64_t batch, int lag,

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/rsp.h"
 #include "rsp_internal.h"
@@ -323,6 +324,169 @@ __global__ __launch_bounds__(kThreads) void hits_kernel(const uint8_t* __restric
     }
 }
 
+// ---- banded hit lists (opt-in, see measure_bands): several workgroups per CPI, each owning
+// a band of Vb rows, in three launches -- band counts per column, one scan per CPI in find()
+// order (column, then band), band lists with those offsets -- meant for batches below the CU
+// count, where one workgroup per CPI leaves most of the chip idle.
+
+// Per-column hit counts of band `band`: cnt[(cpi * R + c) * nb + band] (scan order).
+template <int CW>
+__global__ __launch_bounds__(kThreads) void band_count_kernel(const uint8_t* __restrict__ flag, int V, int R, int G,
+                                                              int64_t ld, int64_t cs, int nb, int Vb,
+                                                              int32_t* __restrict__ cnt) {
+    __shared__ int s_cnt[kThreads * CW];
+    const int cpi = blockIdx.x / nb, band = blockIdx.x - cpi * nb;
+    const uint8_t* fl = flag + cpi * cs;
+    const int S = kThreads / G;
+    const int g = threadIdx.x % G, s = threadIdx.x / G;
+    const int b_lo = band * Vb, b_hi = min(V, b_lo + Vb);
+    const int rows = (b_hi - b_lo + S - 1) / S;
+    const int v_lo = min(b_hi, b_lo + s * rows), v_hi = min(b_hi, v_lo + rows);
+    int32_t* out = cnt + (size_t)cpi * R * nb + band;
+    for (int c_pass = 0; c_pass < R; c_pass += G * CW) {
+        const int c0 = c_pass + g * CW;
+        int c_[CW];
+#pragma unroll
+        for (int j = 0; j < CW; ++j) c_[j] = 0;
+        if (c0 < R) {
+#pragma unroll 4
+            for (int v = v_lo; v < v_hi; ++v) {
+                const uint32_t pat = row_pattern<CW>(fl, (size_t)v * ld + c0);
+#pragma unroll
+                for (int j = 0; j < CW; ++j) c_[j] += (pat >> j) & 1u;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < CW; ++j) s_cnt[(g * CW + j) * S + s] = c_[j];
+        __syncthreads();
+        for (int k = threadIdx.x; k < G * CW; k += kThreads) {
+            const int c = c_pass + k;
+            if (c < R) {
+                int t = 0;
+                for (int q = 0; q < S; ++q) t += s_cnt[k * S + q];
+                out[(size_t)c * nb] = t;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// One workgroup per CPI: the band counts become exclusive offsets in find() order (scan index
+// c * nb + band), in place; count[cpi] = {total, 0}.
+__global__ __launch_bounds__(kThreads) void band_scan_kernel(int R, int nb, int32_t* __restrict__ cnt,
+                                                             int32_t* __restrict__ count) {
+    __shared__ int s_wave[33];
+    const int cpi = blockIdx.x;
+    int32_t* base = cnt + (size_t)cpi * nb * R;
+    const int64_t n = (int64_t)R * nb;
+    const int64_t per = (n + kThreads - 1) / kThreads;
+    const int64_t lo = min(n, (int64_t)threadIdx.x * per), hi = min(n, lo + per);
+    int part = 0;
+    for (int64_t k = lo; k < hi; ++k) part += base[k];   // contiguous chunk: loads issued together
+    int total;
+    int pre = block_scan(part, s_wave, &total);
+    for (int64_t k = lo; k < hi; ++k) {
+        const int x = base[k];
+        base[k] = pre;
+        pre += x;
+    }
+    if (threadIdx.x == 0) {
+        count[cpi * 2 + 0] = total;
+        count[cpi * 2 + 1] = 0;
+    }
+}
+
+// The hits of band `band` into their slots: off[band][c] + the rows of column c above this
+// thread's slice within the band.
+template <int E, int CW>
+__global__ __launch_bounds__(kThreads) void band_list_kernel(const uint8_t* __restrict__ flag, int V, int R, int G,
+                                                             int64_t ld, int64_t cs, int nb, int Vb, int mtd0_num,
+                                                             const int32_t* __restrict__ off, int64_t max_hits,
+                                                             double* __restrict__ est, int32_t* __restrict__ count) {
+    __shared__ int s_cnt[kThreads * CW];
+    __shared__ int s_start[kThreads * CW];
+    __shared__ int s_wave[33];
+    __shared__ int s_bad;
+    const int cpi = blockIdx.x / nb, band = blockIdx.x - cpi * nb;
+    const uint8_t* fl = flag + cpi * cs;
+    int64_t* hl = reinterpret_cast<int64_t*>(est) + (size_t)cpi * max_hits * 3;
+    const int32_t* bo = off + (size_t)cpi * R * nb + band;   // column c at bo[c * nb]
+    const int S = kThreads / G;
+    const int g = threadIdx.x % G, s = threadIdx.x / G;
+    const int b_lo = band * Vb, b_hi = min(V, b_lo + Vb);
+    const int rows = (b_hi - b_lo + S - 1) / S;
+    const int v_lo = min(b_hi, b_lo + s * rows), v_hi = min(b_hi, v_lo + rows);
+    const int q = (rows + 63) / 64;
+    if (threadIdx.x == 0) s_bad = 0;
+    for (int c_pass = 0; c_pass < R; c_pass += G * CW) {
+        const int c0 = c_pass + g * CW;
+        int c_[CW];
+#pragma unroll
+        for (int j = 0; j < CW; ++j) c_[j] = 0;
+        uint64_t rmask = 0;
+        if (c0 < R) {
+#pragma unroll 4
+            for (int v = v_lo; v < v_hi; ++v) {
+                const uint32_t pat = row_pattern<CW>(fl, (size_t)v * ld + c0);
+#pragma unroll
+                for (int j = 0; j < CW; ++j) c_[j] += (pat >> j) & 1u;
+                rmask |= (uint64_t)(pat != 0) << ((v - v_lo) / q);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < CW; ++j) s_cnt[(g * CW + j) * S + s] = c_[j];
+        __syncthreads();
+        int run[CW], part = 0;
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+            run[j] = s_cnt[threadIdx.x * CW + j];
+            part += run[j];
+        }
+        int total;
+        int pre = block_scan(part, s_wave, &total);
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+            const int x = run[j];
+            s_cnt[threadIdx.x * CW + j] = pre;   // within-band prefix P(column, slice)
+            pre += x;
+        }
+        __syncthreads();
+        // slot starts into a second array (P(column, 0) of other slices must stay readable)
+#pragma unroll 1
+        for (int j = 0; j < CW; ++j) {
+            const int k = g * CW + j, c = c_pass + k;
+            s_start[k * S + s] = c < R ? bo[(size_t)c * nb] + s_cnt[k * S + s] - s_cnt[k * S] : 0;
+        }
+        __syncthreads();
+        while (rmask) {
+            const int i = __builtin_ctzll(rmask);
+            rmask &= rmask - 1;
+            const int r_hi = min(v_hi, v_lo + (i + 1) * q);
+            for (int v = v_lo + i * q; v < r_hi; ++v) {
+                uint32_t pat = row_pattern<CW>(fl, (size_t)v * ld + c0);
+                while (pat) {
+                    const int j = __builtin_ctz(pat);
+                    pat &= pat - 1;
+                    const int c = c0 + j;
+                    int* nx = &s_start[(g * CW + j) * S + s];
+                    const int slot = *nx;
+                    *nx = slot + 1;
+                    if (slot < max_hits) {
+                        hl[(size_t)slot * 3] = (int64_t)v * R + c;
+                    } else {
+                        int f0;
+                        if (!fix_cells(c + 1, E, 1, R, R, &f0) ||
+                            !fix_cells(v + 1, E, mtd0_num + 2, V - mtd0_num, V, &f0))
+                            atomicAdd(&s_bad, 1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && s_bad) atomicAdd(&count[cpi * 2 + 1], s_bad);
+}
+
 // One thread per listed hit (nb blocks per CPI): the cell index hits_kernel left in the first
 // word of the slot is replaced by the slot's three estimates.
 template <int E>
@@ -355,41 +519,71 @@ __global__ __launch_bounds__(256) void measure_kernel(const float* __restrict__ 
 template <int E>
 hipError_t launch_e(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
                     const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
-                    double* est, int32_t* cells, int32_t* count, hipStream_t st) {
+                    double* est, int32_t* cells, int32_t* count, int32_t* band_cnt, int nb, hipStream_t st) {
     const bool wide = R % 16 == 0 && R >= 16 * 16 && a.ld % 16 == 0 && a.cs % 16 == 0 && ((uintptr_t)flag & 15) == 0;
     // column groups per pass: a power of two covering the columns (16-byte groups: at least 16,
     // one 256-byte row segment per 16 lanes; bytes: at least 64), at most 1024
     int G = wide ? 16 : 64;
     const int groups = wide ? R / 16 : R;
     while (G < groups && G < kThreads) G <<= 1;
-    if (wide)
+    if (nb > 1) {   // banded: nb workgroups per CPI
+        const int Vb = (V + nb - 1) / nb;
+        const unsigned grid = (unsigned)((int64_t)batch * nb);
+        if (wide)
+            hipLaunchKernelGGL((band_count_kernel<16>), dim3(grid), dim3(kThreads), 0, st, flag, V, R, G, a.ld, a.cs,
+                               nb, Vb, band_cnt);
+        else
+            hipLaunchKernelGGL((band_count_kernel<1>), dim3(grid), dim3(kThreads), 0, st, flag, V, R, G, a.ld, a.cs,
+                               nb, Vb, band_cnt);
+        hipLaunchKernelGGL(band_scan_kernel, dim3(batch), dim3(kThreads), 0, st, R, nb, band_cnt, count);
+        if (wide)
+            hipLaunchKernelGGL((band_list_kernel<E, 16>), dim3(grid), dim3(kThreads), 0, st, flag, V, R, G, a.ld,
+                               a.cs, nb, Vb, a.mtd0_num, band_cnt, max_hits, est, count);
+        else
+            hipLaunchKernelGGL((band_list_kernel<E, 1>), dim3(grid), dim3(kThreads), 0, st, flag, V, R, G, a.ld,
+                               a.cs, nb, Vb, a.mtd0_num, band_cnt, max_hits, est, count);
+    } else if (wide) {
         hipLaunchKernelGGL((hits_kernel<E, 16>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.ld, a.cs, a.mtd0_num,
                            max_hits, est, count);
-    else
+    } else {
         hipLaunchKernelGGL((hits_kernel<E, 1>), dim3(batch), dim3(kThreads), 0, st, flag, V, R, G, a.ld, a.cs, a.mtd0_num,
                            max_hits, est, count);
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess || max_hits == 0) return err;
     // slots past a CPI's hit count exit at once; the grid covers max_hits (capped by V*R)
     const int64_t cap = max_hits < (int64_t)V * R ? max_hits : (int64_t)V * R;
-    const int64_t nb = (cap + 255) / 256, blocks = nb * batch;   // blocks per CPI, total (1-D grid)
+    const int64_t nbk = (cap + 255) / 256, blocks = nbk * batch;   // blocks per CPI, total (1-D grid)
     if (blocks > 0x7fffffff) return hipErrorInvalidConfiguration;
     hipLaunchKernelGGL((measure_kernel<E>), dim3((unsigned)blocks), dim3(256), 0, st, sum, diff, V, R, a, r_scale,
-                       v_scale, max_hits, est, cells, count, (unsigned)nb);
+                       v_scale, max_hits, est, cells, count, (unsigned)nbk);
     return hipGetLastError();
 }
 
 }  // namespace
 
+// Opt-in (RSP_MEASURE_BANDS=N > 1, A/B): N bands per CPI for batches below the CU count.
+// Measured slower than one workgroup per CPI at every batch tried (2048 x 512, ~1044 hits:
+// batch 1 113 vs 64 us, batch 8 84 vs 65 us, batch 64 100 vs 79 us per call): its three
+// launches each cost more than the single workgroup's whole flag scan (band_scan alone 50 us
+// of dependent loads in one workgroup).  Bit-exact against the oracle when enabled.
+int measure_bands(int V, int batch) {
+    static const char* env = getenv("RSP_MEASURE_BANDS");
+    const int want = env ? atoi(env) : 1;
+    if (want <= 1 || batch >= 128) return 1;
+    const int max_nb = (V + 31) / 32;                      // bands of at least 32 rows
+    return want < max_nb ? want : max_nb;
+}
+
 hipError_t launch_measure(const float* sum, const float* diff, const uint8_t* flag, int V, int R, int batch,
                           const MeasureArgs& a, const double* r_scale, const double* v_scale, int64_t max_hits,
-                          double* est, int32_t* cells, int32_t* count, hipStream_t st) {
+                          double* est, int32_t* cells, int32_t* count, int32_t* band_cnt, int nb, hipStream_t st) {
     if (batch <= 0) return hipSuccess;
     switch (a.extra_dots) {
-        case 1: return launch_e<1>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, st);
-        case 2: return launch_e<2>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, st);
-        case 3: return launch_e<3>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, st);
-        case 4: return launch_e<4>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, st);
+        case 1: return launch_e<1>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, band_cnt, nb, st);
+        case 2: return launch_e<2>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, band_cnt, nb, st);
+        case 3: return launch_e<3>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, band_cnt, nb, st);
+        case 4: return launch_e<4>(sum, diff, flag, V, R, batch, a, r_scale, v_scale, max_hits, est, cells, count, band_cnt, nb, st);
         default: return hipErrorInvalidValue;
     }
 }

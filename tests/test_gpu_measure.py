@@ -49,8 +49,8 @@ def _run(meas, s, d, f, kw, max_hits=None):
     return est.cpu().numpy(), cells.cpu().numpy(), count.cpu().numpy()
 
 
-def _check(est, cells, count, s, d, f, kw):
-    for b in range(s.shape[0]):
+def _check(est, cells, count, s, d, f, kw, cpis=None):
+    for b in (range(s.shape[0]) if cpis is None else cpis):
         re, ve, el, hc = mr.motion_para_measure(s[b].astype(np.float64), d[b].astype(np.float64), f[b],
                                                 on_error="nan", **kw)
         n = len(re)
@@ -74,6 +74,19 @@ def test_measure_parity(meas, e, V, R):
     est, cells, count = _run(meas, s, d, f, kw)
     _check(est, cells, count, s, d, f, kw)
     assert count[:, 0].min() > 20 and count[:, 1].min() >= 1     # the band hits at row 0 / V-1 fail
+
+
+@pytest.mark.parametrize("V,R", [(64, 256), (96, 250)])
+def test_measure_large_batch_path(meas, V, R):
+    """batch >= 128: one workgroup per CPI (hits_kernel); smaller batches above run the banded
+    path (band_count / band_scan / band_list).  Same bit-exact bar on a sample of CPIs, and
+    every CPI's count equals its flag total."""
+    rng = np.random.default_rng(V + R)
+    s, d, f = _scene(rng, 130, V, R, 0.002)
+    kw = _kw(2, 5, R, V)
+    est, cells, count = _run(meas, s, d, f, kw)
+    assert (count[:, 0] == f.reshape(130, -1).sum(1)).all()
+    _check(est, cells, count, s, d, f, kw, cpis=(0, 1, 64, 127, 128, 129))
 
 
 def test_measure_dense_and_truncated(meas):
