@@ -204,6 +204,9 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
+#ifndef RSP_FIR_RELOAD
+#define RSP_FIR_RELOAD 0   // 1: re-read all 7 window values per tap group (A/B)
+#endif
 template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t) {
@@ -240,16 +243,31 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
     for (int m0 = 4 * t; m0 < len; m0 += 4 * G) {
         float2 acc[4] = {};
         const float2* p = s2 + kp + m0;     // p[i] = x[m0 + i]
+        float2 w[7];                         // w[q] = x[m0 + q - 3 - k]
+#if RSP_FIR_RELOAD
         for (int k = 0; k < g.ntaps4; k += 4) {
-            float2 w[7];                     // w[q] = x[m0 + q - 3 - k]
 #pragma unroll
             for (int q = 0; q < 7; ++q) w[q] = p[q - 3 - k];
+#else
+        // w[4..6] of tap group k+4 are w[0..2] of group k: 4 LDS reads per group instead of 7
+        w[4] = p[1];
+        w[5] = p[2];
+        w[6] = p[3];
+        for (int k = 0; k < g.ntaps4; k += 4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = p[q - 3 - k];
+#endif
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 const float2 b = taps[k + kk];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i - kk + 3], b, acc[i]);
             }
+#if !RSP_FIR_RELOAD
+            w[6] = w[2];
+            w[5] = w[1];
+            w[4] = w[0];
+#endif
         }
         if (valid) {
 #pragma unroll
