@@ -207,6 +207,16 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
 #ifndef RSP_FIR_RELOAD
 #define RSP_FIR_RELOAD 0   // 1: re-read all 7 window values per tap group (A/B)
 #endif
+// RSP_FIR_PAD: stage the segment with one pad slot per group of 4 (element i at i + i/4).
+// A tap group's 4 window reads are one aligned group (kp - 3 and k are multiples of 4), so
+// they stay contiguous while the lane stride grows from 32 to 40 bytes (fewer bank conflicts).
+#ifndef RSP_FIR_PAD
+#define RSP_FIR_PAD 0   // measured neutral at c3 (250.2k vs 251.4k CPI/s, bit-exact); DESIGN.md §7
+#endif
+#if RSP_FIR_PAD && RSP_FIR_RELOAD
+#error "RSP_FIR_PAD needs the window-reuse FIR (RSP_FIR_RELOAD=0)"
+#endif
+__device__ __forceinline__ int fir_slot(int i) { return RSP_FIR_PAD ? i + (i >> 2) : i; }
 template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t) {
@@ -230,12 +240,12 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             }
 #pragma unroll
             for (int q = 0; q < B; ++q)
-                if (i0 + q * G < nst) s2[i0 + q * G] = v[q];
+                if (i0 + q * G < nst) s2[fir_slot(i0 + q * G)] = v[q];
         }
     } else {
         for (int i = t; i < nst; i += G) {
             const int j = i - kp;
-            s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+            s2[fir_slot(i)] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
         }
     }
     xsync<WS>();
@@ -248,6 +258,17 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
         for (int k = 0; k < g.ntaps4; k += 4) {
 #pragma unroll
             for (int q = 0; q < 7; ++q) w[q] = p[q - 3 - k];
+#elif RSP_FIR_PAD
+        // As below, on the padded staging: w[0..3] of group k are padded group gb - k/4
+        const int gb = (kp + m0 - 3) >> 2;
+        (void)p;
+        w[4] = s2[5 * (gb + 1)];
+        w[5] = s2[5 * (gb + 1) + 1];
+        w[6] = s2[5 * (gb + 1) + 2];
+        for (int k = 0; k < g.ntaps4; k += 4) {
+            const float2* pg = s2 + 5 * (gb - (k >> 2));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = pg[q];
 #else
         // w[4..6] of tap group k+4 are w[0..2] of group k: 4 LDS reads per group instead of 7
         w[4] = p[1];
@@ -816,7 +837,8 @@ bool pc_mf_supported(int nfft, int fir_stage_len) {
     switch (nfft) {
         case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: case 8192:
         case 16384:
-            return fir_stage_len <= padded_len(nfft);   // the FIR stages its input in the row's slot
+            // the FIR stages its input in the row's slot (padded: element i at i + i/4)
+            return (RSP_FIR_PAD ? fir_stage_len + fir_stage_len / 4 + 1 : fir_stage_len) <= padded_len(nfft);
         default:
             return false;
     }
