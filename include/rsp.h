@@ -29,7 +29,10 @@
  *     host buffers, the context owns its device buffers (grow-only pool).
  *   - _dev entry points take device pointers and enqueue on `stream` (a hipStream_t,
  *     NULL = the null stream); they return before the work completes.
- *   - One context per host thread and device.  MATLAB calls MEX on one thread.
+ *   - One context per host thread and device.  MATLAB calls MEX on one thread.  Contexts
+ *     on different threads and devices are independent (kernel launch setup is cached per
+ *     device, thread-safely).  _dev calls on one context may use different streams: each
+ *     call's stream first waits for the previous call's use of the context's scratch.
  *   - Device layouts are row-major C order: echo [batch][P][R] complex (interleaved
  *     I/Q), RDM [batch][Nd][R_out] float32, flags [batch][Nd][R_out] uint8 0/1, where
  *     Nd = P (Doppler bins) and R_out = params.R_out.
@@ -230,7 +233,9 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
  * windows, P = 128 with the 1024 + 4096-point v2 segment pair), rsp_pc_mtd_cfar_dev and the
  * host entry points run PC -> MTD -> CFAR of the whole call as ONE persistent launch, with
  * the corner turn through a small ring of scratch CPIs instead of a chunk-sized scratch.
- * enable = 0 selects the chunked two-kernel pipeline.  Results are bit-identical. */
+ * enable = 0 selects the chunked two-kernel pipeline.  Results are bit-identical.
+ * The in-kernel waits are bounded: _dev results of a fused call are valid only once
+ * rsp_chain_check returns RSP_OK (the host-buffer entry points check it themselves). */
 int rsp_set_fused(rsp_ctx* ctx, int32_t enable);
 /* Waits for the context's work and reports whether a fused launch gave up waiting for an
  * item (a bounded in-kernel wait that expired): RSP_ERR_HIP with a message if so. */

@@ -49,7 +49,7 @@ def lib():
                                C.c_int, C.c_int, C.c_int, C.c_double,
                                C.c_int, C.c_int, C.c_int, C.c_double,
                                C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                               C.c_void_p, C.c_void_p, C.c_int]
+                               C.c_void_p, C.c_void_p, C.c_double, C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -129,22 +129,28 @@ def pc_mtd(echo, pre, nthreads=0):
     return out
 
 
-def cfar(rdm, c, segments, nthreads=0):
+def cfar(rdm, c, segments, nthreads=0, near_tol=None):
     """main_cfar chain on [batch, V, R]: optional /div 0-v then fun_CFARflag.
-    c: dict with refR saveR TR methodR refV saveV TV methodV M0 rFlag zero_v_div."""
+    c: dict with refR saveR TR methodR refV saveV TV methodV M0 rFlag zero_v_div.
+    Returns (flag, flagV), or (flag, flagV, ambiguous) with near_tol (the rules of
+    rsp_ref.executeCFAR(near_tol))."""
     r = np.ascontiguousarray(np.asarray(rdm, np.float64))
     if r.ndim == 2:
         r = r[None]
     B, V, R = r.shape
     flag = np.empty((B, V, R), np.uint8)
     flagV = np.empty((B, V, R), np.uint8)
+    amb = np.empty((B, V, R), np.uint8) if near_tol is not None else None
     n = len(segments)
     lo = np.array([s[0] for s in segments] or [0], np.int64)
     hi = np.array([s[1] for s in segments] or [R], np.int64)
     rc = lib().orc_cfar(r.ctypes.data, B, V, R, c["refR"], c["saveR"], c["methodR"], float(c["TR"]),
                         c["refV"], c["saveV"], c["methodV"], float(c["TV"]), c["M0"], c["rFlag"],
                         c.get("zero_v_div", 0), n, lo.ctypes.data, hi.ctypes.data,
-                        flag.ctypes.data, flagV.ctypes.data, int(nthreads))
+                        flag.ctypes.data, flagV.ctypes.data, float(near_tol or 0.0),
+                        amb.ctypes.data if amb is not None else None, int(nthreads))
     if rc:
         raise RuntimeError("orc_cfar failed: %d (a CFAR window does not fit)" % rc)
+    if amb is not None:
+        return flag, flagV, amb.astype(bool)
     return flag, flagV

@@ -52,6 +52,31 @@ static long next_pow2(long n) {
     return p;
 }
 
+/* Twiddle table W_n^k = exp(-2 pi i k / n), k < n/2, computed in fp64 once per length and
+   thread (a small per-thread cache: the PC rows and MTD columns of a call reuse 2-3 lengths). */
+#define ORC_TW_CACHE 4
+typedef struct {
+    long n;
+    cplx* w;
+} orc_tw;
+static __thread orc_tw tw_cache[ORC_TW_CACHE];
+static __thread int tw_next;
+
+static const cplx* twiddles(long n) {
+    for (int i = 0; i < ORC_TW_CACHE; ++i)
+        if (tw_cache[i].n == n) return tw_cache[i].w;
+    orc_tw* e = &tw_cache[tw_next];
+    tw_next = (tw_next + 1) % ORC_TW_CACHE;
+    free(e->w);
+    e->n = n;
+    e->w = malloc(sizeof(cplx) * (size_t)(n / 2 > 0 ? n / 2 : 1));
+    for (long k = 0; k < n / 2; ++k) {
+        const double ang = -2.0 * M_PI * (double)k / (double)n;
+        e->w[k] = cos(ang) + I * sin(ang);
+    }
+    return e->w;
+}
+
 /* in-place iterative radix-2, sign -1 forward / +1 inverse (unscaled) */
 static void fft2(cplx* a, long n, int sign) {
     for (long i = 1, j = 0; i < n; ++i) {
@@ -64,31 +89,61 @@ static void fft2(cplx* a, long n, int sign) {
             a[j] = t;
         }
     }
+    const cplx* tw = twiddles(n);
     for (long len = 2; len <= n; len <<= 1) {
-        const double ang = sign * 2.0 * M_PI / (double)len;
-        for (long k = 0; k < len / 2; ++k) {
-            const cplx w = cos(ang * k) + I * sin(ang * k);
-            for (long i = 0; i < n; i += len) {
-                const cplx u = a[i + k], v = a[i + k + len / 2] * w;
+        const long half = len / 2, step = n / len;
+        for (long i = 0; i < n; i += len) {
+            for (long k = 0; k < half; ++k) {
+                const cplx w = sign < 0 ? tw[k * step] : conj(tw[k * step]);
+                const cplx u = a[i + k], v = a[i + k + half] * w;
                 a[i + k] = u + v;
-                a[i + k + len / 2] = u - v;
+                a[i + k + half] = u - v;
             }
         }
     }
 }
 
-/* any n: radix-2 when possible, direct DFT otherwise (oracle: correctness over speed) */
+/* exp(sign 2 pi i e / n) with the exponent reduced mod n first (exact phase) */
+static cplx cis_mod(long e, long n, int sign) {
+    const double ang = sign * 2.0 * M_PI * (double)(e % n) / (double)n;
+    return cos(ang) + I * sin(ang);
+}
+
+/* Forward DFT matrix W_n^{km} of a length without a radix plan (e.g. the v2 native P = 332),
+   one per thread, built once in fp64 from reduced exponents. */
+static __thread long dftm_n;
+static __thread cplx* dftm;
+
+/* any n (tmp: n entries): radix-2 for 2^k; 3 * 2^k as three decimated radix-2 transforms
+   combined with exact twiddles, X[k] = sum_r W_n^{rk} F_r[k mod m] (the DMX / legacy 1536);
+   a DFT-matrix product otherwise (oracle: correctness over speed) */
 static void dft_any(cplx* a, long n, int sign, cplx* tmp) {
     if (is_pow2(n)) {
         fft2(a, n, sign);
         return;
     }
-    for (long k = 0; k < n; ++k) {
-        cplx s = 0;
-        for (long m = 0; m < n; ++m) {
-            const double ang = sign * 2.0 * M_PI * (double)((k * m) % n) / (double)n;
-            s += a[m] * (cos(ang) + I * sin(ang));
+    if (n % 3 == 0 && is_pow2(n / 3)) {
+        const long m = n / 3;
+        for (int r = 0; r < 3; ++r)
+            for (long j = 0; j < m; ++j) tmp[r * m + j] = a[3 * j + r];
+        for (int r = 0; r < 3; ++r) fft2(tmp + r * m, m, sign);
+        for (long k = 0; k < n; ++k) {
+            const long km = k % m;
+            a[k] = tmp[km] + cis_mod(k, n, sign) * tmp[m + km] + cis_mod(2 * k, n, sign) * tmp[2 * m + km];
         }
+        return;
+    }
+    if (dftm_n != n) {
+        free(dftm);
+        dftm = malloc(sizeof(cplx) * (size_t)n * n);
+        for (long k = 0; k < n; ++k)
+            for (long j = 0; j < n; ++j) dftm[k * n + j] = cis_mod(k * j, n, -1);
+        dftm_n = n;
+    }
+    for (long k = 0; k < n; ++k) {
+        const cplx* w = dftm + k * n;
+        cplx s = 0;
+        for (long j = 0; j < n; ++j) s += a[j] * (sign < 0 ? w[j] : conj(w[j]));
         tmp[k] = s;
     }
     memcpy(a, tmp, sizeof(cplx) * (size_t)n);
@@ -222,10 +277,16 @@ static int side_avg(const double* line, long st, long n, long y, int ref, int sa
     return 1;
 }
 
-/* executeCFAR on the column block [c0, c1) of one RDM ([V][Rt], row stride Rt). */
+/* Relative margin of a CFAR decision |x - thr| / |thr| (inf / NaN at thr == 0, as numpy). */
+static double margin(double x, double thr) { return fabs(x - thr) / fabs(thr); }
+
+/* executeCFAR on the column block [c0, c1) of one RDM ([V][Rt], row stride Rt).
+   amb (nullable): the near-threshold mask of SURVEY.md §8d with the rules of
+   oracle/rsp_ref.py executeCFAR(near_tol): output cells that could flip under a relative
+   perturbation of near_tol of the RDM. */
 static int execute_cfar(const double* rdm, long V, long Rt, long c0, long c1, int refR, int saveR, int methodR,
                         double TR, int refV, int saveV, int methodV, double TV, int M0, int rFlag,
-                        unsigned char* flag, unsigned char* flagV) {
+                        unsigned char* flag, unsigned char* flagV, double near_tol, unsigned char* amb) {
     const long lo = M0 + 1, hi = V - M0, nv = hi - lo, nr = c1 - c0;   /* rows M0+2 : V-M0  (:23) */
     if (nv <= 0) return -2;
     /* Doppler CFAR: Function_CFAR1D_sub(used.') slides along Doppler for every range bin (:28) */
@@ -234,6 +295,12 @@ static int execute_cfar(const double* rdm, long V, long Rt, long c0, long c1, in
             double avg;
             if (!side_avg(rdm + lo * Rt + r, Rt, nv, v - lo, refV, saveV, methodV, &avg)) return -3;
             flagV[v * Rt + r] = rdm[v * Rt + r] >= avg * TV;    /* :45-46 */
+            if (amb && margin(rdm[v * Rt + r], avg * TV) < near_tol) {
+                /* flag = flagV: the cell itself; range stage: a hit at r reaches r-1..r+1 */
+                const long a0 = rFlag ? (r - 1 > c0 ? r - 1 : c0) : r;
+                const long a1 = rFlag ? (r + 1 < c1 - 1 ? r + 1 : c1 - 1) : r;
+                for (long c = a0; c <= a1; ++c) amb[v * Rt + c] = 1;
+            }
         }
     }
     if (!rFlag) {   /* :91 */
@@ -249,6 +316,9 @@ static int execute_cfar(const double* rdm, long V, long Rt, long c0, long c1, in
             const long rr = r - c0;
             long best = -1;
             double bx = 0;
+            int near = 0;
+            double top1 = -INFINITY, top2 = -INFINITY;   /* the two largest candidate values */
+            int ncell = 0;
             for (long c = rr - 1; c <= rr + 1; ++c) {   /* r-1 : r+1 within [1, rCellNum] (:50-57) */
                 if (c < 0 || c >= nr) continue;
                 double avg;
@@ -259,8 +329,22 @@ static int execute_cfar(const double* rdm, long V, long Rt, long c0, long c1, in
                         bx = row[c];
                     }
                 }
+                ++ncell;
+                if (margin(row[c], avg * TR) < near_tol) near = 1;
+                if (row[c] > top1) {
+                    top2 = top1;
+                    top1 = row[c];
+                } else if (row[c] > top2) {
+                    top2 = row[c];
+                }
             }
             if (best >= 0) flag[v * Rt + c0 + best] = 1;   /* :78-84 */
+            if (amb) {   /* a near-threshold candidate, or a near tie for the first maximum */
+                if (ncell > 1 && top1 > 0 && (top1 - top2) / top1 < near_tol) near = 1;
+                if (near)
+                    for (long c = rr - 1; c <= rr + 1; ++c)
+                        if (c >= 0 && c < nr) amb[v * Rt + c0 + c] = 1;
+            }
         }
     }
     return 0;
@@ -270,7 +354,8 @@ static int execute_cfar(const double* rdm, long V, long Rt, long c0, long c1, in
    column segment).  rdm [batch][V][R]; flag/flagV [batch][V][R] uint8. */
 int orc_cfar(const double* rdm, long batch, long V, long R, int refR, int saveR, int methodR, double TR,
              int refV, int saveV, int methodV, double TV, int M0, int rFlag, int zero_v_div, int nseg,
-             const long* seg_lo, const long* seg_hi, unsigned char* flag, unsigned char* flagV, int nthreads) {
+             const long* seg_lo, const long* seg_hi, unsigned char* flag, unsigned char* flagV, double near_tol,
+             unsigned char* amb, int nthreads) {
     long zlo, zhi;
     zero_band(V, zero_v_div, &zlo, &zhi);
     int err = 0;
@@ -288,12 +373,14 @@ int orc_cfar(const double* rdm, long batch, long V, long R, int refR, int saveR,
             for (long v = zlo; v < zhi; ++v) memset(m + v * R, 0, sizeof(double) * (size_t)R);
             unsigned char* f = flag + (size_t)b * V * R;
             unsigned char* fv = flagV + (size_t)b * V * R;
+            unsigned char* am = amb ? amb + (size_t)b * V * R : NULL;
             memset(f, 0, (size_t)V * R);
             memset(fv, 0, (size_t)V * R);
+            if (am) memset(am, 0, (size_t)V * R);
             for (int s = 0; s < (nseg > 0 ? nseg : 1); ++s) {
                 const long c0 = nseg > 0 ? seg_lo[s] : 0, c1 = nseg > 0 ? seg_hi[s] : R;
                 int rc = execute_cfar(m, V, R, c0, c1, refR, saveR, methodR, TR, refV, saveV, methodV, TV, M0, rFlag,
-                                      f, fv);
+                                      f, fv, near_tol, am);
                 if (rc) err = rc;
             }
         }

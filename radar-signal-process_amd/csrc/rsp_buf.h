@@ -64,10 +64,7 @@ __device__ __forceinline__ void buf_st_f_stream(float v, __amdgpu_buffer_rsrc_t 
 // bypassed, no acquire fence), with one agent-scope counter add per producing workgroup
 // after all its waves drained vmcnt (cdna_hip_programming.md Guideline 16, valid-form row 1).
 // Aux template argument: 0 = default policy, kSc1 = write-through / L1-bypass.
-#ifndef RSP_AB_HANDOFF_AUX
-#define RSP_AB_HANDOFF_AUX 16
-#endif
-constexpr int kSc1 = RSP_AB_HANDOFF_AUX;   // (ablation builds may set 0: plain, NOT coherent)
+constexpr int kSc1 = 16;   // aux bits of a cross-workgroup hand-off access (sc1: write-through / re-fetch)
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 

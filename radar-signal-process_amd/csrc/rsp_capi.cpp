@@ -44,6 +44,11 @@ struct rsp_ctx {
     int nstreams = 2;   // chunk pipelines (the caller's stream + nstreams-1 internal ones)
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+    // The context's scratch (PC corner turn, hit lists, internal RDM, flagV staging) is reused by
+    // every _dev call: a call's stream waits for the previous call's release event first, so
+    // calls on different streams never overlap on it.
+    hipEvent_t ev_scratch = nullptr;
+    bool scratch_pending = false;
     std::vector<void*> owned;           // constant tables (freed at destroy)
     std::map<int, float2*> tw;          // twiddle tables by length
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
@@ -217,6 +222,7 @@ int rsp_destroy(rsp_ctx* ctx) {
         if (ctx->ev_join[i]) hipEventDestroy(ctx->ev_join[i]);
     }
     if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_scratch) hipEventDestroy(ctx->ev_scratch);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return RSP_OK;
@@ -652,6 +658,18 @@ static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_
 
 static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess; }
 
+// Order this call's use of the context scratch after the previous call's (on any stream).
+static int scratch_acquire(rsp_ctx* ctx, hipStream_t s) {
+    if (ctx->scratch_pending) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_scratch, 0));
+    return RSP_OK;
+}
+static int scratch_release(rsp_ctx* ctx, hipStream_t s) {
+    if (!ctx->ev_scratch) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_scratch, hipEventDisableTiming));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_scratch, s));
+    ctx->scratch_pending = true;
+    return RSP_OK;
+}
+
 static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s);
 
 // Run one kernel launch, bracketed by HIP events on `s` when profiling is on (every
@@ -822,9 +840,9 @@ static int run_fused(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t nc
 // win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
 // frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
 // frames plus the look-ahead frame once, and every window reads its rows from that PC.
-static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
-                     const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                     float* d_diff, hipStream_t s, bool pc_input = false) {
+static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
+                          const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                          float* d_diff, hipStream_t s, bool pc_input) {
     const int64_t P = ctx->p.P, R = ctx->p.R, Ro = ctx->p.R_out, V = ctx->V, NB = ctx->beams;
     const size_t esz = dtype == RSP_C64 ? 8 : 4;
     rsp::MtdArgs m = ctx->mtd;
@@ -957,6 +975,16 @@ static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t un
     return RSP_OK;
 }
 
+static int run_chain(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
+                     const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                     float* d_diff, hipStream_t s, bool pc_input = false) {
+    int rc = scratch_acquire(ctx, s);
+    if (rc) return rc;
+    rc = run_chain_body(ctx, d_echo, dtype, units, win, cfar, d_rdm, d_flag, d_flagV, d_diff, s, pc_input);
+    if (rc) return rc;
+    return scratch_release(ctx, s);
+}
+
 static int check_chain_args(rsp_ctx* ctx, const char* fn, const void* d_echo, int32_t dtype, int64_t n,
                             const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "%s: null ctx", fn);
@@ -1030,16 +1058,22 @@ int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_cfar_dev: null ctx");
     if (!d_rdm || !cfar || !d_flag || V < 1 || R < 1 || batch < 0)
         return fail(ctx, RSP_ERR_ARG, "rsp_cfar_dev: bad argument");
-    if ((V + 1) * 4 > 64 * 1024 || R * 6 > 150 * 1024)
+    if ((V + 1) * 4 > 64 * 1024 || R > (1 << 24))
         return fail(ctx, RSP_ERR_UNSUPPORTED, "rsp_cfar_dev: V=%lld or R=%lld too large", (long long)V, (long long)R);
-    if (batch == 0) return RSP_OK;
-    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
     rsp::CfarVArgs cv;
     rsp::CfarRArgs cr;
     int rc = build_cfar(ctx, cfar, V, R, &cv, &cr);
     if (rc) return rc;
+    if (!rsp::cfar_r_supported(cr))
+        return fail(ctx, RSP_ERR_UNSUPPORTED,
+                    "rsp_cfar_dev: a %lld-cell row with range window ref=%d guard=%d needs more than 160 KB of LDS "
+                    "(only ref=5, guard=7 with R %% 4 == 0 is built for rows over 16320 cells)",
+                    (long long)R, cr.ref, cr.save);
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
     hipStream_t s = (hipStream_t)stream;
     const int64_t chunk = 65535;
+    if ((rc = scratch_acquire(ctx, s))) return rc;
     if (!d_flagV) {
         rc = ensure(ctx, ctx->tmp_flagV, (size_t)(batch < chunk ? batch : chunk) * V * R);
         if (rc) return rc;
@@ -1052,7 +1086,7 @@ int rsp_cfar_dev(rsp_ctx* ctx, const float* d_rdm, int64_t V, int64_t R, int64_t
         HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_V, s, [&] { return rsp::launch_cfar_v(rdm, fv, (int)n, (int)V, (int)R, cv, s); }));
         HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, s, [&] { return rsp::launch_cfar_r(rdm, fv, fl, (int)n, cr, s); }));
     }
-    return RSP_OK;
+    return scratch_release(ctx, s);
 }
 
 // ------------------------------------------------------------------ post-detection measurement
@@ -1098,14 +1132,16 @@ int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff
     a.ele_comp = mp->ele_comp;
     a.ele_sys_err = mp->ele_sys_err;
     const int nb = rsp::measure_bands((int)V, (int)batch);
+    int rc = scratch_acquire(ctx, (hipStream_t)stream);
+    if (rc) return rc;
     if (nb > 1) {
-        const int rc = ensure(ctx, ctx->meas_band, (size_t)batch * nb * R * sizeof(int32_t));
+        rc = ensure(ctx, ctx->meas_band, (size_t)batch * nb * R * sizeof(int32_t));
         if (rc != RSP_OK) return rc;
     }
     HIP_TRY(ctx, rsp::launch_measure(d_sum, d_diff, d_flag, (int)V, (int)R, (int)batch, a, d_r_scale, d_v_scale,
                                      max_hits, d_est, d_cells, d_count, (int32_t*)ctx->meas_band.p, nb,
                                      (hipStream_t)stream));
-    return RSP_OK;
+    return scratch_release(ctx, (hipStream_t)stream);
 }
 
 // ------------------------------------------------------------------ echo pre-filters
@@ -1275,6 +1311,7 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
             return rc;
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->fused) return rsp_chain_check(ctx);   // a fused launch whose bounded wait expired is an error
     return RSP_OK;
 }
 

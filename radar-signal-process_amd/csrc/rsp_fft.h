@@ -339,12 +339,10 @@ __device__ __forceinline__ void fft_reg(float2 (&u)[E], float2* buf, int t, cons
             float2 v[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) v[r] = u[i + r * PER];
-#ifndef RSP_AB_NOTW
             if constexpr (Ns > 1) {
                 const int k = (t + i * G) % Ns;
                 twiddle<R, N>(v, k * (N / (Ns * R)), tw);
             }
-#endif
             dft<R>(v);
 #pragma unroll
             for (int r = 0; r < R; ++r) u[i + r * PER] = v[r];

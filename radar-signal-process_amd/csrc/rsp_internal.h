@@ -4,11 +4,35 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/rsp.h"
 
 namespace rsp {
 
 constexpr int kBlock = 256;  // threads per workgroup for every kernel (4 waves of 64)
+
+// One-time launch setup of a kernel (hipFuncSetAttribute, occupancy -> resident grid), per
+// device: both apply to the calling thread's current device, and contexts on different host
+// threads and devices launch concurrently (rsp.h threading model), so the setup runs once per
+// (kernel, device) under std::call_once and its result is cached per device.
+constexpr int kMaxDevices = 64;
+struct LaunchOnce {
+    std::once_flag once[kMaxDevices];
+    hipError_t err[kMaxDevices] = {};
+    int value[kMaxDevices] = {};
+};
+// init(dev, &value) -> hipError_t; *value receives the cached value (e.g. resident workgroups)
+template <typename F>
+inline hipError_t launch_once(LaunchOnce& L, int* value, F&& init) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    std::call_once(L.once[dev], [&] { L.err[dev] = init(dev, &L.value[dev]); });
+    if (value) *value = L.value[dev];
+    return L.err[dev];
+}
 
 // One pulse-compression segment as the kernel sees it (see rsp_pc_segment).
 struct SegDev {
@@ -208,6 +232,9 @@ void mtd_regions(int P, int R_out, int ncpi, int* nregions, int* region, int bea
 int mtd_bluestein_nf(int P);
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
                          const CfarRArgs& a, hipStream_t s);
+// Whether launch_cfar_r has a kernel for the row length / window (the generic kernel stages a
+// row in LDS: 10 bytes per cell)
+bool cfar_r_supported(const CfarRArgs& a);
 // dtype/layout conversion of a host-API input into [batch][P][R] complex float32.
 hipError_t launch_ingest(const void* in, int dtype, int layout, float2* out, int64_t batch,
                          int P, int R, hipStream_t s);

@@ -121,16 +121,16 @@ size_t pc_lds_bytes(int max_nfft) { return (size_t)padded_len(max_nfft < 64 ? 64
 hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, const PcArgs& a,
                      size_t lds_bytes, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)pc_kernel<float2>,
+    static LaunchOnce once;
+    hipError_t e = launch_once(once, nullptr, [](int, int*) {
+        hipError_t r = hipFuncSetAttribute((const void*)pc_kernel<float2>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)pc_kernel<__half2>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+        if (r == hipSuccess)
+            r = hipFuncSetAttribute((const void*)pc_kernel<__half2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024);
+        return r;
+    });
+    if (e != hipSuccess) return e;
     dim3 grid((unsigned)rows), block(kBlock);
     if (dtype == RSP_C64) {
         hipLaunchKernelGGL(pc_kernel<float2>, grid, block, lds_bytes, s, (const float2*)echo, out, a);
@@ -142,30 +142,6 @@ hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, con
     return hipGetLastError();
 }
 
-// ================================================================== diagnostic stamps
-// -DRSP_STAMPS builds record s_memtime at phase boundaries of the first NSTAMP_BLOCKS
-// long-segment PC blocks (thread 0); read back with rsp_debug_stamps().  Never in the
-// product build.
-#ifdef RSP_STAMPS
-constexpr int kStampSlots = 8, kStampBlocks = 8192;
-__device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define RSP_STAMP(slot)                                                                    \
-    do {                                                                                   \
-        if (stamp_on) {                                                                    \
-            unsigned long long t_ = stamp_now();                                           \
-            if (threadIdx.x == 0) g_stamps[stamp_blk * kStampSlots + (slot)] = t_;         \
-        }                                                                                  \
-    } while (0)
-#else
-#define RSP_STAMP(slot) do { } while (0)
-#endif
 
 // ================================================================== pulse compression v2
 // One launch per matched-filter segment, specialised on its FFT length N: G threads per
@@ -173,20 +149,11 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // 256..512-thread workgroup.  Row loads and stores are lane-contiguous (the strided
 // element pattern of fft_reg), the spectrum multiply sits between the forward and the
 // inverse FFT in registers, and the only LDS traffic is the inter-pass exchange.
-#ifndef RSP_PC_WIDE_N
-#define RSP_PC_WIDE_N 16384
-#endif
-#ifndef RSP_PC_E
-#define RSP_PC_E 16
-#endif
-#ifndef RSP_PC_WAVES
-#define RSP_PC_WAVES 2
-#endif
 template <int N>
 struct PcCfg {
     // 16 elements per thread; 32 from 16384 points on, so a row is 512 threads (2 waves per
     // SIMD, a 256-VGPR budget) instead of 1024 (128 VGPRs: the preloaded twiddles spill)
-    static constexpr int G = N / (N >= RSP_PC_WIDE_N ? 32 : RSP_PC_E);   // threads per row
+    static constexpr int G = N / (N >= 16384 ? 32 : 16);   // threads per row
     static constexpr int E = N / G;                             // elements per thread
     static constexpr int RPB = G >= 256 ? 1 : 256 / G;          // rows per workgroup
     static constexpr int T = G * RPB;
@@ -204,19 +171,6 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
-#ifndef RSP_FIR_RELOAD
-#define RSP_FIR_RELOAD 0   // 1: re-read all 7 window values per tap group (A/B)
-#endif
-// RSP_FIR_PAD: stage the segment with one pad slot per group of 4 (element i at i + i/4).
-// A tap group's 4 window reads are one aligned group (kp - 3 and k are multiples of 4), so
-// they stay contiguous while the lane stride grows from 32 to 40 bytes (fewer bank conflicts).
-#ifndef RSP_FIR_PAD
-#define RSP_FIR_PAD 0   // measured neutral at c3 (250.2k vs 251.4k CPI/s, bit-exact); DESIGN.md §7
-#endif
-#if RSP_FIR_PAD && RSP_FIR_RELOAD
-#error "RSP_FIR_PAD needs the window-reuse FIR (RSP_FIR_RELOAD=0)"
-#endif
-__device__ __forceinline__ int fir_slot(int i) { return RSP_FIR_PAD ? i + (i >> 2) : i; }
 template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t) {
@@ -240,12 +194,12 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             }
 #pragma unroll
             for (int q = 0; q < B; ++q)
-                if (i0 + q * G < nst) s2[fir_slot(i0 + q * G)] = v[q];
+                if (i0 + q * G < nst) s2[i0 + q * G] = v[q];
         }
     } else {
         for (int i = t; i < nst; i += G) {
             const int j = i - kp;
-            s2[fir_slot(i)] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+            s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
         }
     }
     xsync<WS>();
@@ -254,22 +208,6 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
         float2 acc[4] = {};
         const float2* p = s2 + kp + m0;     // p[i] = x[m0 + i]
         float2 w[7];                         // w[q] = x[m0 + q - 3 - k]
-#if RSP_FIR_RELOAD
-        for (int k = 0; k < g.ntaps4; k += 4) {
-#pragma unroll
-            for (int q = 0; q < 7; ++q) w[q] = p[q - 3 - k];
-#elif RSP_FIR_PAD
-        // As below, on the padded staging: w[0..3] of group k are padded group gb - k/4
-        const int gb = (kp + m0 - 3) >> 2;
-        (void)p;
-        w[4] = s2[5 * (gb + 1)];
-        w[5] = s2[5 * (gb + 1) + 1];
-        w[6] = s2[5 * (gb + 1) + 2];
-        for (int k = 0; k < g.ntaps4; k += 4) {
-            const float2* pg = s2 + 5 * (gb - (k >> 2));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = pg[q];
-#else
         // w[4..6] of tap group k+4 are w[0..2] of group k: 4 LDS reads per group instead of 7
         w[4] = p[1];
         w[5] = p[2];
@@ -277,18 +215,15 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
         for (int k = 0; k < g.ntaps4; k += 4) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) w[q] = p[q - 3 - k];
-#endif
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 const float2 b = taps[k + kk];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i - kk + 3], b, acc[i]);
             }
-#if !RSP_FIR_RELOAD
             w[6] = w[2];
             w[5] = w[1];
             w[4] = w[0];
-#endif
         }
         if (valid) {
 #pragma unroll
@@ -322,11 +257,6 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     // loads after the forward FFT (32 fewer live VGPRs across it).
     constexpr bool kEarly = G <= 64;
     if constexpr (kUniform) row = __builtin_amdgcn_readfirstlane(row);
-#ifdef RSP_STAMPS
-    const bool stamp_on = (N == 4096) && blockIdx.x < kStampBlocks;
-    const int stamp_blk = blockIdx.x;
-#endif
-    RSP_STAMP(0);
     const bool valid = row < a.rows;
     const TIn* x = echo + (size_t)row * a.R;
     float2* y = out + (size_t)row * a.R_out;
@@ -342,13 +272,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     if constexpr (kUniform) {
         const auto xr = buf_rsrc(x + in_start, valid ? (uint32_t)in_len * ES : 0u);
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-#ifdef RSP_AB_NOLOAD
-            u[m] = make_float2((float)(t + G * m + row), a.mf.scale);
-#else
-            u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
-#endif
-        }
+        for (int m = 0; m < E; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
     } else {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
@@ -361,48 +285,30 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #pragma unroll
         for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
     }
-#ifndef RSP_AB_NOFIR
     if (a.do_fir) {
-#else
-    if (false) {
-#endif
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
                 for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) st_c<SA>(y + c, make_float2(0.f, 0.f));
         fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
     }
-#ifdef RSP_STAMPS
-    if (stamp_on) { float acc = 0.f; for (int m = 0; m < E; ++m) acc += u[m].x; asm volatile("" :: "v"(acc)); }
-#endif
-    RSP_STAMP(1);
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
-    RSP_STAMP(2);
-#ifndef RSP_AB_NOH
     if constexpr (kEarly) {
 #pragma unroll
         for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hs[m]);   // conj(X.*H), 1/N in H
     } else {
-#ifndef RSP_HB
-#define RSP_HB 8
-#endif
+        constexpr int HB = 8;
 #pragma unroll
-        for (int m0 = 0; m0 < E; m0 += RSP_HB) {
-            float2 h[RSP_HB];   // batches of spectrum loads, then the multiply
+        for (int m0 = 0; m0 < E; m0 += HB) {
+            float2 h[HB];   // batches of spectrum loads, then the multiply
 #pragma unroll
-            for (int m = 0; m < RSP_HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * (m0 + m)) * 8u);
+            for (int m = 0; m < HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * (m0 + m)) * 8u);
 #pragma unroll
-            for (int m = 0; m < RSP_HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
+            for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
         }
     }
-#endif
-    RSP_STAMP(3);
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
-    RSP_STAMP(4);
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
-#ifdef RSP_AB_NOSTORE
-        if (u[0].x == 12345.678f)
-#endif
 #pragma unroll
         for (int m = 0; m < E; ++m) buf_st_f2a<SA>(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
     } else if (valid) {
@@ -412,10 +318,6 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             if (i < out_len) st_c<SA>(y + out_start + i, cconj(u[m]));
         }
     }
-#ifdef RSP_STAMPS
-    if (stamp_on) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    RSP_STAMP(5);
 }
 
 // Workgroup size shared by a pair of segment lengths: both run T threads (RPB = T/G rows).
@@ -432,7 +334,7 @@ struct PairCfg {
 // Single segment (N2 == 0) or two independent segments in one launch: blocks
 // [0, nblk2) run segment 2 (the long one, first for a short tail), the rest segment 1.
 template <typename TIn, int N1, int N2>
-__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_PC_WAVES) void pc_mf_kernel(
+__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_kernel(
     const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
@@ -445,9 +347,6 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_PC_WAVES) voi
             return;
         }
     }
-#ifdef RSP_AB_NOSEG1
-    if (N2 != 0) return;
-#endif
     constexpr int G = PcCfg<N1>::G;
     const int grp = threadIdx.x / G, t = threadIdx.x % G;
     const int b = (int)blockIdx.x - (N2 ? nblk2 : 0);
@@ -468,43 +367,28 @@ __device__ __forceinline__ void mf_load(float2 (&u)[N / G], const TIn* __restric
     constexpr uint32_t ES = sizeof(TIn);
     const auto xr = buf_rsrc(echo + (size_t)row * a.R + a.mf.in_start, valid ? (uint32_t)a.mf.in_len * ES : 0u);
 #pragma unroll
-    for (int m = 0; m < N / G; ++m) {
-#ifdef RSP_AB_NOLOAD
-        u[m] = make_float2((float)(t + G * m + row), a.mf.scale);
-#else
-        u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
-#endif
-    }
+    for (int m = 0; m < N / G; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
 }
 
 template <int N, int G>
 __device__ __forceinline__ void mf_store(const float2 (&u)[N / G], float2* __restrict__ out, const PcMfArgs& a,
                                          int row, int t) {
     const auto yr = buf_rsrc(out + (size_t)row * a.R_out + a.mf.out_start, (uint32_t)a.mf.out_len * 8u);
-#ifdef RSP_AB_NOSTORE
-    if (u[0].x == 12345.678f)
-#endif
 #pragma unroll
     for (int m = 0; m < N / G; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
 }
 
-#ifndef RSP_PC_SHORT_WS
-#define RSP_PC_SHORT_WS 1
-#endif
 // The short-segment groups of a persistent PC workgroup: items first, +gridDim.x, ... < nitems.
 template <typename TIn, int N1, int N2>
 __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, float2* __restrict__ out,
                                                const PcMfArgs& a1, int n2, int nitems, int first, float2* lds) {
-#ifdef RSP_AB_NOSEG1
-    return;
-#endif
     using PC = PairCfg<N1, N2>;
     constexpr int G1 = PcCfg<N1>::G;
     const int grp = threadIdx.x / G1, t1 = threadIdx.x % G1;
     // G1 == 64: a short row is one wave with its own LDS slot, so its exchanges need only the
-    // wave's own ordering (RSP_PC_SHORT_WS): the four rows of a group no longer wait for each
-    // other at every FFT pass
-    constexpr bool WS = RSP_PC_SHORT_WS && G1 == 64;
+    // wave's own ordering: the four rows of a group no longer wait for each other at every
+    // FFT pass
+    constexpr bool WS = G1 == 64;
     if constexpr (WS) __syncthreads();   // the long rows' last LDS reads are done
     for (int item = first; item < nitems; item += (int)gridDim.x) {
         if constexpr (!WS) __syncthreads();   // the previous item's last LDS reads are done
@@ -512,20 +396,8 @@ __device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, flo
     }
 }
 
-#ifndef RSP_PC_LEAN
-#define RSP_PC_LEAN 0
-#endif
-#ifndef RSP_PC_PER_CU
-#define RSP_PC_PER_CU 0   // persistent PC workgroups per CU (0: as many as fit)
-#endif
-#ifndef RSP_PERSIST_WAVES
-#define RSP_PERSIST_WAVES (RSP_PC_LEAN ? 4 : 2)
-#endif
-#ifndef RSP_PC_DEPTH
-#define RSP_PC_DEPTH 1   // long rows in flight ahead of the one being transformed (1 or 2)
-#endif
 template <typename TIn, int N1, int N2>
-__global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_persist_kernel(
+__global__ __launch_bounds__((PairCfg<N1, N2>::T), 2) void pc_persist_kernel(
     const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int n2, int nitems) {
     using PC = PairCfg<N1, N2>;
     static_assert(PcCfg<N2>::G == PC::T, "one long-segment row per workgroup");
@@ -546,44 +418,6 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
         constexpr int NW = tw_regs<N2, E>() > 0 ? tw_regs<N2, E>() : 1;
         const int t = threadIdx.x;
         if (shorts_first) __syncthreads();   // the short items' last LDS reads are done
-#if RSP_PC_LEAN
-        // Lean register plan (for 4 resident workgroups per CU): twiddles and the spectrum
-        // slice are re-loaded per row instead of living in registers for the whole launch.
-        // Load issue order keeps every wait off the younger loads (vmcnt is in order):
-        //   [fwd FFT: twiddles tf] -> issue ti -> multiply (H) -> issue next row -> IFFT (ti)
-        //   -> wait next row -> issue tf, H for the next row -> stores
-        // so the peak live set is u + 2 of {twiddles, H, next row} (~90 VGPRs + temporaries).
-        const auto hr = buf_rsrc(a2.mf.H, (uint32_t)N2 * 8u);
-        float2 u[E], tf[NW], hh[E];
-        mf_load<TIn, N2, G>(u, echo, a2, item, true, t);
-#pragma unroll
-        for (int m = 0; m < E; ++m) asm volatile("" ::"v"(u[m]));
-        tw_preload<N2, G, 1, E, 0, NW>(tf, t, a2.mf.tw);
-#pragma unroll
-        for (int m = 0; m < E; ++m) hh[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-        while (item < n2) {
-            const int next = item + (int)gridDim.x;
-            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, tf);
-            float2 ti[NW];
-            tw_preload<N2, G, 1, E, 0, NW>(ti, t, a2.mf.tw);
-#pragma unroll
-            for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hh[m]);   // conj(X.*H), 1/N in H
-            float2 nx[E];
-            mf_load<TIn, N2, G>(nx, echo, a2, next < n2 ? next : item, next < n2, t);
-            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, ti);
-#pragma unroll
-            for (int m = 0; m < E; ++m) asm volatile("" ::"v"(nx[m]));
-            if (next < n2) {
-                tw_preload<N2, G, 1, E, 0, NW>(tf, t, a2.mf.tw);
-#pragma unroll
-                for (int m = 0; m < E; ++m) hh[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-            }
-            mf_store<N2, G>(u, out, a2, item, t);
-#pragma unroll
-            for (int m = 0; m < E; ++m) u[m] = nx[m];
-            item = next;
-        }
-#else
         float2 w[NW];
         tw_preload<N2, G, 1, E, 0, NW>(w, t, a2.mf.tw);
         float2 h[E];
@@ -592,42 +426,6 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
         for (int m = 0; m < E; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
         float2 u[E];
         mf_load<TIn, N2, G>(u, echo, a2, item, true, t);
-#if RSP_PC_DEPTH == 2
-        // Two rows in flight: three register buffers rotate (row item, item+grid loaded,
-        // item+2*grid loading), unrolled three times so no buffer is ever copied -- a copy
-        // would make the compiler wait for the youngest loads at the end of every row.  Each
-        // row's loads are issued after the forward FFT of the row two steps earlier, so they
-        // have ~1.5 rows of work to land; before a row's stores only the OLDER prefetch is
-        // waited for (vmcnt is in order), the younger one stays in flight.
-        float2 b1[E], b2[E];
-        {
-            const int nx1 = item + (int)gridDim.x;
-            mf_load<TIn, N2, G>(b1, echo, a2, nx1 < n2 ? nx1 : item, nx1 < n2, t);
-        }
-#pragma unroll
-        for (int m = 0; m < E; ++m) asm volatile("" ::"v"(u[m]), "v"(h[m]));
-        const int gs = (int)gridDim.x;
-        auto step = [&](float2 (&cur)[E], float2 (&pf)[E], const float2 (&older)[E]) {
-            fft_reg_w<N2, G, 1, E, 0, NW>(cur, lds, t, w);
-            const int nx2 = item + 2 * gs;
-            mf_load<TIn, N2, G>(pf, echo, a2, nx2 < n2 ? nx2 : item, nx2 < n2, t);
-#pragma unroll
-            for (int m = 0; m < E; ++m) cur[m] = cmul_conj(cur[m], h[m]);   // conj(X.*H), 1/N in H
-            fft_reg_w<N2, G, 1, E, 0, NW>(cur, lds, t, w);
-#pragma unroll
-            for (int m = 0; m < E; ++m) asm volatile("" ::"v"(older[m]));
-            mf_store<N2, G>(cur, out, a2, item, t);
-            item += gs;
-        };
-        for (;;) {
-            if (item >= n2) break;
-            step(u, b2, b1);
-            if (item >= n2) break;
-            step(b1, u, b2);
-            if (item >= n2) break;
-            step(b2, b1, u);
-        }
-#else
         // settle the entry loads here, so the loop header carries no pending load (a merged
         // wait state would put a vmcnt(0) -- a store drain -- at the top of every iteration)
 #pragma unroll
@@ -650,157 +448,44 @@ __global__ __launch_bounds__((PairCfg<N1, N2>::T), RSP_PERSIST_WAVES) void pc_pe
             for (int m = 0; m < E; ++m) u[m] = nx[m];
             item = next;
         }
-#endif
-#endif   // RSP_PC_LEAN
     }
     if (!shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
 }
 
-#ifndef RSP_PC_WAVE
-#define RSP_PC_WAVE 0   // the 1024 + 4096 pair as one wave per row (pc_wave_kernel): measured slower
-#endif
-// ---------------------------------------------------------------- one wave per 4096-point row
-// The 4096-point matched filter as a 64 x 64 four-step transform owned by ONE wave: lane t
-// holds x[t + 64m] (m < 64, 128 VGPRs), and
-//   pass 1: DFT64 over m in registers -> Y[t][k1]; twiddle W4096^{t k1};
-//   corner turn through the wave's LDS slot (lane t writes row t, lane k reads column k);
-//   pass 2: DFT64 over n1 in registers -> X[k1 + 64 k2] in register k2 (natural order: the
-//   input pattern of the inverse transform, of the spectrum loads and of coalesced stores).
-// No workgroup barrier anywhere (a wave's LDS operations are performed in issue order) and one
-// LDS exchange per transform instead of two.  The corner turn moves the real and the
-// imaginary halves in turn through a 64 x 65-float slot (16.6 KB per wave), so two workgroups
-// of four waves fit a CU.  Short-segment rows (FIR + N1-point MF) run one row per wave too.
-constexpr int kWaveStride = 65;                  // floats per slot row (odd: b32 row writes and column reads conflict-free)
-constexpr int kWaveSlot = 64 * kWaveStride;      // floats per wave
-
-// twiddle bases of lane t: B[i] = W4096^{t i}, A[j] = W4096^{8 t j} (i, j < 8), from the table
-// (offsets recomputed per call: an opaque lane copy keeps them from being hoisted out of the
-// row loop, where 16 loop-invariant addresses would be spilled)
-__device__ __forceinline__ void tw4096_bases(float2 (&A)[8], float2 (&B)[8], const float2* __restrict__ tw, int lane) {
-    const auto tr = buf_rsrc(tw, 4096u * 8u);
-    uint32_t l8 = (uint32_t)lane * 8u;
-    asm volatile("" : "+v"(l8));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        B[i] = buf_ld_f2(tr, l8 * (uint32_t)i, 0u);
-        A[i] = buf_ld_f2(tr, l8 * (uint32_t)(8 * i), 0u);
-    }
-}
-
-// Y[t][m] *= W4096^{t m} = A[m / 8] * B[m % 8]
-__device__ __forceinline__ void tw4096(float2 (&v)[64], const float2 (&A)[8], const float2 (&B)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i == 0 && j == 0) continue;
-            const float2 w = (j == 0) ? B[i] : (i == 0 ? A[j] : cmul(A[j], B[i]));
-            v[8 * j + i] = cmul(v[8 * j + i], w);
-        }
-    }
-}
-
-// corner turn: lane t's v[m] = Y[t][m]  ->  lane k's v[n] = Y[n][k]; real halves, then imaginary
-__device__ __forceinline__ void turn64(float2 (&v)[64], float* slot, int lane) {
-    float* row = slot + lane * kWaveStride;
-#pragma unroll
-    for (int m = 0; m < 64; ++m) row[m] = v[m].x;
-    xsync<true>();
-#pragma unroll
-    for (int n = 0; n < 64; ++n) v[n].x = slot[n * kWaveStride + lane];
-    xsync<true>();
-#pragma unroll
-    for (int m = 0; m < 64; ++m) row[m] = v[m].y;
-    xsync<true>();
-#pragma unroll
-    for (int n = 0; n < 64; ++n) v[n].y = slot[n * kWaveStride + lane];
-    xsync<true>();
-}
-
-__device__ __forceinline__ void fft4096_wave(float2 (&v)[64], float* slot, int lane, const float2* __restrict__ tw) {
-    float2 A[8], B[8];
-    tw4096_bases(A, B, tw, lane);   // table loads (L1/L2 hits) land during the first DFT64
-    dft64(v);
-    tw4096(v, A, B);
-    turn64(v, slot, lane);
-    dft64(v);
-}
-
-// One long-segment row (4096-point matched filter) by one wave.
-template <typename TIn>
-__device__ __forceinline__ void pc_long_wave(const TIn* __restrict__ echo, float2* __restrict__ out,
-                                             const PcMfArgs& a, int row, int lane, float* slot) {
-    constexpr uint32_t ES = sizeof(TIn);
-    row = __builtin_amdgcn_readfirstlane(row);
-    const auto xr = buf_rsrc(echo + (size_t)row * a.R + a.mf.in_start, (uint32_t)a.mf.in_len * ES);
-    float2 v[64];
-#pragma unroll
-    for (int m = 0; m < 64; ++m) v[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)lane * ES, (uint32_t)(64 * m) * ES);
-    fft4096_wave(v, slot, lane, a.mf.tw);
-    const auto hr = buf_rsrc(a.mf.H, 4096u * 8u);
-#pragma unroll
-    for (int m0 = 0; m0 < 64; m0 += 16) {
-        float2 h[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) h[m] = buf_ld_f2(hr, (uint32_t)lane * 8u, (uint32_t)(64 * (m0 + m)) * 8u);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m0 + m] = cmul_conj(v[m0 + m], h[m]);   // conj(X.*H), 1/N in H
-    }
-    fft4096_wave(v, slot, lane, a.mf.tw);
-    const auto yr = buf_rsrc(out + (size_t)row * a.R_out + a.mf.out_start, (uint32_t)a.mf.out_len * 8u);
-#pragma unroll
-    for (int m = 0; m < 64; ++m) buf_st_f2(cconj(v[m]), yr, (uint32_t)lane * 8u, (uint32_t)(64 * m) * 8u);
-}
-
-// Items gw, gw + nw, ... of the launch's 2*rows: [0, rows) long rows, [rows, 2 rows) short rows.
-template <typename TIn, int N1>
-#ifndef RSP_PC_WAVE_WPS
-#define RSP_PC_WAVE_WPS 2   // waves per SIMD the register budget is sized for (1: 512 incl. AGPRs)
-#endif
-__global__ __launch_bounds__(256, RSP_PC_WAVE_WPS) void pc_wave_kernel(const TIn* __restrict__ echo, float2* __restrict__ out,
-                                                         PcMfArgs a1, PcMfArgs a2, int rows) {
-    static_assert(PcCfg<N1>::G == 64 && (size_t)padded_len(N1) * 2 <= (size_t)kWaveSlot, "short row = one wave");
-    extern __shared__ __attribute__((aligned(16))) float lds_f[];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* slot = lds_f + wv * kWaveSlot;
-    const int gw = (int)blockIdx.x * 4 + wv, nw = (int)gridDim.x * 4;
-    for (int item = gw; item < 2 * rows; item += nw) {
-        // an opaque lane copy per item: lane-derived addresses are recomputed inside the item
-        // instead of being hoisted out of the loop (and spilled)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        if (item < rows) pc_long_wave<TIn>(echo, out, a2, item, ln, slot);
-        else pc_row<TIn, N1, 64, 0, true>(echo, out, a1, item - rows, ln, reinterpret_cast<float2*>(slot));
-    }
-}
-
-static int device_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-    }
+static int device_cus(int dev) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     return cus;
+}
+
+// Resident workgroups of a persistent kernel on the current device (once per device).
+static hipError_t resident_grid(LaunchOnce& once, const void* kernel, int threads, size_t lds, int* resident) {
+    return launch_once(once, resident, [&](int dev, int* out) {
+        hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds);
+        if (e != hipSuccess) return e;
+        *out = (per_cu > 0 ? per_cu : 1) * device_cus(dev);
+        return hipSuccess;
+    });
+}
+
+// Dynamic-LDS attribute of a kernel (once per device).
+static hipError_t lds_attr(LaunchOnce& once, const void* kernel, size_t lds) {
+    return launch_once(once, nullptr, [&](int, int*) {
+        return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
 }
 
 template <typename TIn, int N1, int N2>
 static hipError_t launch_pc_persist(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs& a2,
                                     hipStream_t s) {
     using PC = PairCfg<N1, N2>;
-    static int resident = 0;
-    if (!resident) {
-        hipError_t e = hipFuncSetAttribute((const void*)pc_persist_kernel<TIn, N1, N2>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)PC::lds);
-        if (e != hipSuccess) return e;
-        int per_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_persist_kernel<TIn, N1, N2>,
-                                                         PC::T, PC::lds);
-        if (e != hipSuccess) return e;
-        if (RSP_PC_PER_CU > 0 && RSP_PC_PER_CU < per_cu) per_cu = RSP_PC_PER_CU;   // A/B: leave CU room to MTD
-        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
-    }
+    static LaunchOnce once;
+    int resident = 0;
+    hipError_t e = resident_grid(once, (const void*)pc_persist_kernel<TIn, N1, N2>, PC::T, PC::lds, &resident);
+    if (e != hipSuccess) return e;
     const int n2 = a1.rows;                                  // one item per long-segment row
     const int nitems = n2 + (a1.rows + PC::RPB1 - 1) / PC::RPB1;
     const int grid = nitems < resident ? nitems : resident;
@@ -809,36 +494,12 @@ static hipError_t launch_pc_persist(const TIn* echo, float2* out, const PcMfArgs
     return hipGetLastError();
 }
 
-#if RSP_PC_WAVE
-template <typename TIn, int N1>
-static hipError_t launch_pc_wave(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs& a2,
-                                 hipStream_t s) {
-    constexpr size_t lds = (size_t)4 * kWaveSlot * sizeof(float);
-    static int resident = 0;
-    if (!resident) {
-        hipError_t e = hipFuncSetAttribute((const void*)pc_wave_kernel<TIn, N1>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        int per_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_wave_kernel<TIn, N1>, 256, lds);
-        if (e != hipSuccess) return e;
-        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
-    }
-    const int rows = a1.rows;
-    const int want = (2 * rows + 3) / 4;
-    const int grid = want < resident ? want : resident;
-    if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((pc_wave_kernel<TIn, N1>), dim3((unsigned)grid), dim3(256), lds, s, echo, out, a1, a2, rows);
-    return hipGetLastError();
-}
-#endif
-
 bool pc_mf_supported(int nfft, int fir_stage_len) {
     switch (nfft) {
         case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: case 8192:
         case 16384:
-            // the FIR stages its input in the row's slot (padded: element i at i + i/4)
-            return (RSP_FIR_PAD ? fir_stage_len + fir_stage_len / 4 + 1 : fir_stage_len) <= padded_len(nfft);
+            // the FIR stages its input in the row's slot
+            return fir_stage_len <= padded_len(nfft);
         default:
             return false;
     }
@@ -849,13 +510,9 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
                                  hipStream_t s) {
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)pc_mf_kernel<TIn, N1, N2>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)PC::lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static LaunchOnce once;
+    hipError_t e = lds_attr(once, (const void*)pc_mf_kernel<TIn, N1, N2>, PC::lds);
+    if (e != hipSuccess) return e;
     const int nblk1 = (a1.rows + PC::RPB1 - 1) / PC::RPB1;
     const int nblk2 = N2 ? (a1.rows + PC::RPB2 - 1) / PC::RPB2 : 0;
     dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
@@ -864,24 +521,11 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     return hipGetLastError();
 }
 
-#ifndef RSP_PC_PERSIST
-#define RSP_PC_PERSIST 1
-#endif
-#ifndef RSP_PC_PERSIST8K
-#define RSP_PC_PERSIST8K 1   // the persistent kernel for the 1024 + 8192 pair (c4: PC 314 -> 185 us per launch)
-#endif
-#if RSP_PC_WAVE
-#define RSP_PC_WAVE_LAUNCH(n1, n2) if (n2 == 4096) return launch_pc_wave<TIn, n1>(echo, out, a1, *a2, s);
-#else
-#define RSP_PC_WAVE_LAUNCH(n1, n2)
-#endif
 #define RSP_PAIR(n1, n2) \
     if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s)
 #define RSP_PAIR_PERSIST(n1, n2)                                                              \
     if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) {                                        \
-        RSP_PC_WAVE_LAUNCH(n1, n2)                                                            \
-        if (RSP_PC_PERSIST) return launch_pc_persist<TIn, n1, n2>(echo, out, a1, *a2, s);     \
-        return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s);                             \
+        return launch_pc_persist<TIn, n1, n2>(echo, out, a1, *a2, s);                         \
     }
 
 template <typename TIn>
@@ -890,11 +534,7 @@ static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a
     // fused pairs of the built-in presets (v2 at 1024..16384 range bins, legacy)
     RSP_PAIR(1024, 1024);
     RSP_PAIR_PERSIST(1024, 4096);
-#if RSP_PC_PERSIST8K
-    RSP_PAIR_PERSIST(1024, 8192);
-#else
-    RSP_PAIR(1024, 8192);
-#endif
+    RSP_PAIR_PERSIST(1024, 8192);   // c4: PC 314 -> 185 us per launch against pc_mf_kernel
     RSP_PAIR(1024, 16384);
     RSP_PAIR(512, 1024);
     if (a2) return hipErrorNotSupported;
@@ -1003,20 +643,10 @@ struct MtdCfg {
     // elements per thread: 32 from P = 512 on (one beam), so a tile keeps >= 16 range bins
     // (>= 128-B row segments) as P grows; 16 below and for the two-beam pair (whose second
     // beam's magnitudes already take E registers); 24 for the 3*2^k lengths
-#ifndef RSP_MTD_WIDE
-#define RSP_MTD_WIDE 1
-#endif
-#ifndef RSP_MTD_E_SMALL
-#define RSP_MTD_E_SMALL 16   // elements per thread for 2^k lengths below 512 (A/B knob)
-#endif
-    static constexpr int E = (P % 3 == 0) ? 24 : ((RSP_MTD_WIDE && BEAMS == 1 && P >= 512) ? 32 : RSP_MTD_E_SMALL);
+    static constexpr int E = (P % 3 == 0) ? 24 : ((BEAMS == 1 && P >= 512) ? 32 : 16);
     static constexpr int G = P / E;                    // threads per range bin
-    // threads per workgroup: 512 for one-beam P = 256 (32 range bins, 256-B row segments, at
-    // the same LDS per range bin), 256 otherwise
-#ifndef RSP_MTD_WIDE256
-#define RSP_MTD_WIDE256 0   // measured neutral at c4 (529 vs 523 us per launch)
-#endif
-    static constexpr int T = (RSP_MTD_WIDE256 && BEAMS == 1 && P == 256) ? 512 : kBlock;
+    // threads per workgroup (512 for P = 256 measured neutral at c4: 529 vs 523 us per launch)
+    static constexpr int T = kBlock;
     static constexpr int W = T / G;                    // range bins per workgroup
     static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
     static constexpr int MS = P + 1;                   // odd float stride of a CFAR column
@@ -1390,74 +1020,6 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T)) void mtd_kernel(const float2
     mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
 }
 
-// Persistent single-beam MTD (RSP_MTD_PERSIST=1; off: 1.42 vs 1.15 us/CPI for MTD alone at c3,
-// the hardware's workgroup scheduling overlaps tiles better): a resident grid walks the launch's tiles (tile = cpi * nbx + bx,
-// the hit-list region of mtd_kernel's workgroup of the same tile), and each workgroup loads
-// its next tile's samples before it runs the current one's FFT and Doppler CFAR -- the CFAR
-// phase otherwise leaves the workgroup with no memory in flight.  Blocks [0, nprev) run the
-// previous chunk's range stage (dispatched first, as mtd_kernel's row 0).
-#ifndef RSP_MTD_PERSIST
-#define RSP_MTD_PERSIST 0   // measured slower than the one-tile-per-workgroup mtd_kernel
-#endif
-__device__ __forceinline__ void prev_chunk_hits_b(const MtdArgs& a, int b, int nb) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (int)blockDim.x / 64;
-    const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
-    for (int rg = b * nw + w; rg < a.prev_nregions; rg += nb * nw) {
-        if (ref57)
-            cfar_hit_region<5, 7>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
-                                  lane);
-        else
-            cfar_hit_region<0, 0>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
-                                  lane);
-    }
-}
-
-template <int P, int REF>
-__global__ __launch_bounds__((MtdCfg<P>::T), 4) void mtd_persist_kernel(const float2* __restrict__ pc, float* __restrict__ rdm,
-                                                             uint8_t* __restrict__ flagV, MtdArgs a, int ntiles,
-                                                             int nbx, int nprev) {
-    if ((int)blockIdx.x < nprev) {
-        prev_chunk_hits_b(a, blockIdx.x, nprev);
-        return;
-    }
-    using C = MtdCfg<P, 1>;
-    constexpr int E = C::E;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t s_hits;
-    const int nwg = (int)gridDim.x - nprev;
-    int t = (int)blockIdx.x - nprev;
-    if (t >= ntiles) return;
-    const size_t R = (size_t)a.R_out;
-    const size_t plane = (size_t)P * R;
-    auto rows = [&](int tile) {   // first PC row of the tile's CPI
-        const size_t cpi = (size_t)(tile / nbx);
-        return a.nwin > 0 ? (cpi / a.nwin) * (size_t)a.pin + a.win_start[cpi % a.nwin] : cpi * (size_t)a.pin;
-    };
-    float2 u[E];
-    mtd_tile_load<P, 0>(u, pc + rows(t) * R, t % nbx, a, true);
-    while (t < ntiles) {
-        const int tn = t + nwg;
-        float2 nx[E];   // the next tile, in flight during this one
-        mtd_tile_load<P, 0>(nx, pc + rows(tn < ntiles ? tn : t) * R, (tn < ntiles ? tn : t) % nbx, a, tn < ntiles);
-        const size_t cpi = (size_t)(t / nbx);
-        MtdTile T;
-        T.pc = pc + rows(t) * R;
-        T.rdm = rdm + cpi * plane;
-        T.diff = nullptr;
-        T.flagV = flagV ? flagV + cpi * plane : nullptr;
-        T.flag = a.flag ? a.flag + cpi * plane : nullptr;
-        T.hits = a.hits ? a.hits + (size_t)t * (C::W * P) : nullptr;
-        T.hit_count = a.hit_count ? a.hit_count + t : nullptr;
-        T.cell_base = (uint32_t)(cpi * plane);
-        T.bx = t % nbx;
-        mtd_tile<P, REF, 1, 0, 0, true>(T, a, smem, &s_hits, u);
-        __syncthreads();   // the tile's last LDS reads (CFAR) and s_hits store are done
-#pragma unroll
-        for (int m = 0; m < E; ++m) u[m] = nx[m];
-        t = tn;
-    }
-}
-
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
 // MTD/main_produce_dataset_win_xzr_v2.m:31) by Bluestein's identity:
 //   X[k] = c[k] sum_n (x[n] w[n] c[n]) conj(c[k-n]),   c[n] = exp(-j pi n^2 / P),
@@ -1553,13 +1115,9 @@ static hipError_t launch_mtd_bluestein(const float2* pc, float* rdm, uint8_t* fl
     if (a.pin < 2 || 2 * a.pin - 1 > NF || a.beams != 1 || a.shift < 0 || a.shift >= a.pin) return hipErrorInvalidValue;
     if (a.cv.enabled && a.cv.save + a.cv.ref + 2 > C::SPAD) return hipErrorInvalidValue;
     if ((uint64_t)a.pin * a.R_out * 8 >= (uint64_t)kOob) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)mtd_bluestein_kernel<NF>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static LaunchOnce once;
+    hipError_t e = lds_attr(once, (const void*)mtd_bluestein_kernel<NF>, C::lds);
+    if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
         block(C::T);
     hipLaunchKernelGGL((mtd_bluestein_kernel<NF>), grid, block, C::lds, s, pc, rdm, flagV, a);
@@ -1572,45 +1130,14 @@ int mtd_bluestein_nf(int P) {
     return nf <= 2048 ? nf : 0;
 }
 
-template <int P, int REF>
-static hipError_t launch_mtd_persist(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, const MtdArgs& a,
-                                     hipStream_t s) {
-    using C = MtdCfg<P, 1>;
-    constexpr size_t lds = C::template lds_for<REF>();
-    static int resident = 0;
-    if (!resident) {
-        hipError_t e = hipFuncSetAttribute((const void*)mtd_persist_kernel<P, REF>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        int per_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mtd_persist_kernel<P, REF>, C::T, lds);
-        if (e != hipSuccess) return e;
-        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
-    }
-    const int nbx = (a.R_out + C::W - 1) / C::W;
-    const int ntiles = nbx * ncpi;
-    const int nprev = a.prev_nregions > 0 ? nbx : 0;
-    const int nwg = ntiles < resident ? ntiles : resident;
-    if (nwg + nprev < 1) return hipSuccess;
-    hipLaunchKernelGGL((mtd_persist_kernel<P, REF>), dim3((unsigned)(nwg + nprev)), dim3(C::T), lds, s, pc, rdm,
-                       flagV, a, ntiles, nbx, nprev);
-    return hipGetLastError();
-}
-
 template <int P, int REF, int BEAMS>
 static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, int ncpi,
                                 const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P, BEAMS>;
     constexpr size_t lds = C::template lds_for<REF>();
-    if constexpr (RSP_MTD_PERSIST && BEAMS == 1 && C::E == 16)
-        return launch_mtd_persist<P, REF>(pc, rdm, flagV, ncpi, a, s);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)mtd_kernel<P, REF, BEAMS>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static LaunchOnce once;
+    hipError_t e = lds_attr(once, (const void*)mtd_kernel<P, REF, BEAMS>, lds);
+    if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
         block(C::T);
     hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, lds, s, pc, rdm, flagV, a);
@@ -1755,13 +1282,9 @@ hipError_t launch_cfar_v(const float* rdm, uint8_t* flagV, int ncpi, int V, int 
     int lw = 6;
     while (lw > 0 && (size_t)2 * (1 << lw) * (V + 1) * sizeof(float) > 96 * 1024) --lw;
     const size_t lds = (size_t)2 * (1 << lw) * (V + 1) * sizeof(float);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)cfar_v_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static LaunchOnce once;
+    hipError_t e = lds_attr(once, (const void*)cfar_v_kernel, 160 * 1024);
+    if (e != hipSuccess) return e;
     dim3 grid((unsigned)((R + (1 << lw) - 1) >> lw), (unsigned)ncpi), block(kBlock);
     hipLaunchKernelGGL(cfar_v_kernel, grid, block, lds, s, rdm, flagV, V, R, lw, a);
     return hipGetLastError();
@@ -2066,18 +1589,22 @@ hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hit
     return hipGetLastError();
 }
 
+// The window-specialised range kernels need no LDS; cfar_r_generic_kernel stages a row (+ halo)
+// as x, window sums, pass and flagV bytes: 10 bytes per cell (none when rflag == 0: it copies flagV).
+static bool cfar_r_specialised(const CfarRArgs& a) { return a.ref == 5 && a.save == 7 && a.rflag && (a.R & 3) == 0; }
+static size_t cfar_r_generic_lds(const CfarRArgs& a) {
+    return a.rflag ? (size_t)(((a.R + 3) & ~3) + 2 * kHalo) * (2 * sizeof(float) + 2) : 0;
+}
+bool cfar_r_supported(const CfarRArgs& a) { return cfar_r_specialised(a) || cfar_r_generic_lds(a) <= 160 * 1024; }
+
 hipError_t launch_cfar_r(const float* rdm, const uint8_t* flagV, uint8_t* flag, int ncpi,
                          const CfarRArgs& a, hipStream_t s) {
     if (ncpi <= 0) return hipSuccess;
-    const int L = ((a.R + 3) & ~3) + 2 * kHalo;
-    const size_t lds = (size_t)L * (2 * sizeof(float) + 2);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)cfar_r_generic_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    if (!cfar_r_supported(a)) return hipErrorInvalidValue;
+    const size_t lds = cfar_r_generic_lds(a);
+    static LaunchOnce once;
+    hipError_t e = lds_attr(once, (const void*)cfar_r_generic_kernel, 160 * 1024);
+    if (e != hipSuccess) return e;
     if (a.ref == 5 && a.save == 7 && a.rflag && (a.R & 15) == 0) {   // the reference's parameters
         const int groups = (a.R / 16 + kBlock - 1) / kBlock;
         dim3 grid((unsigned)(groups * a.V), (unsigned)ncpi), block(kBlock);
@@ -2201,9 +1728,6 @@ __device__ __forceinline__ uint32_t chain_claim(uint32_t* ctl, int h) {
 // wait that lasts 0.5 s sets the timeout word, and once it is set no wait blocks: the launch
 // then completes with wrong data (reported by rsp_chain_check) instead of hanging the GPU.
 __device__ __forceinline__ void chain_wait(uint32_t* p, uint32_t target, uint32_t* tmo) {
-#ifdef RSP_AB_NOWAIT
-    return;
-#endif
     if (__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -2218,9 +1742,7 @@ __device__ __forceinline__ void chain_wait(uint32_t* p, uint32_t target, uint32_
 
 // Every wave drains its stores, then thread 0 publishes the workgroup's item.
 __device__ __forceinline__ void chain_signal(uint32_t* p) {
-#ifndef RSP_AB_NODRAIN
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2308,7 +1830,7 @@ __device__ __forceinline__ void chain_item(const ChainArgs& a, int h, uint32_t q
 }
 
 template <typename TIn, int N1, int N2, int P, int REF>
-__global__ __launch_bounds__(kBlock, RSP_PERSIST_WAVES) void chain_kernel(ChainArgs a) {
+__global__ __launch_bounds__(kBlock, 2) void chain_kernel(ChainArgs a) {
     using CC = ChainCfg<N1, N2, P>;
     static_assert(CC::PC::T == kBlock && PcCfg<N2>::G == kBlock, "one long-segment row per workgroup");
     static_assert(CC::MC::W * CC::MC::G == kBlock, "MTD tile shape");
@@ -2360,17 +1882,10 @@ __global__ __launch_bounds__(kBlock, RSP_PERSIST_WAVES) void chain_kernel(ChainA
 template <typename TIn, int N1, int N2, int P, int REF>
 static hipError_t launch_chain_t(ChainArgs& a, hipStream_t s) {
     using CC = ChainCfg<N1, N2, P>;
-    static int resident = 0;
-    if (!resident) {
-        hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<TIn, N1, N2, P, REF>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CC::lds);
-        if (e != hipSuccess) return e;
-        int per_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)chain_kernel<TIn, N1, N2, P, REF>,
-                                                         kBlock, CC::lds);
-        if (e != hipSuccess) return e;
-        resident = (per_cu > 0 ? per_cu : 1) * device_cus();
-    }
+    static LaunchOnce once;
+    int resident = 0;
+    hipError_t e = resident_grid(once, (const void*)chain_kernel<TIn, N1, N2, P, REF>, kBlock, CC::lds, &resident);
+    if (e != hipSuccess) return e;
     a.nl = P;
     a.nsh = (P + CC::PC::RPB1 - 1) / CC::PC::RPB1;
     a.nm = (a.a2.R_out + CC::MC::W - 1) / CC::MC::W;
@@ -2409,11 +1924,3 @@ hipError_t launch_chain(int dtype, ChainArgs& a, hipStream_t s) {
 
 }  // namespace rsp
 
-#ifdef RSP_STAMPS
-extern "C" int rsp_debug_stamps(unsigned long long* host, int nblocks) {
-    if (nblocks > rsp::kStampBlocks) nblocks = rsp::kStampBlocks;
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(rsp::g_stamps),
-                                    sizeof(unsigned long long) * rsp::kStampSlots * nblocks, 0,
-                                    hipMemcpyDeviceToHost);
-}
-#endif

@@ -49,13 +49,13 @@ def _targets(spec):
     return out
 
 
-def _clean(spec):
-    """Target + clutter part of one CPI (deterministic, no noise): P x R complex128."""
+def _clean(spec, snr_db=20.0):
+    """Target part of one CPI (deterministic, no noise): P x R complex128."""
     P, R = spec.P, spec.R
     rp = spec.radar
     lam, prt = rp["wavelength"], rp["prt"]
     x = np.zeros((P, R), np.complex128)
-    amp = 10.0 ** (20.0 / 20.0)
+    amp = 10.0 ** (snr_db / 20.0)
     m = np.arange(P)
     for wf, d, v in _targets(spec):
         fd = 2.0 * v / lam
@@ -75,15 +75,17 @@ def _clutter(spec, rng):
     return c
 
 
-def echo_numpy(spec, batch=1, seed=1000, dtype=np.complex64):
-    """[batch, P, R] synthetic echoes; CPI b uses numpy PCG64(seed + b)."""
+def echo_numpy(spec, batch=1, seed=1000, dtype=np.complex64, snr_db=20.0, scale=1.0):
+    """[batch, P, R] synthetic echoes; CPI b uses numpy PCG64(seed + b).  snr_db: target
+    power over the unit noise power; scale multiplies the whole echo (fp16 range sweeps)."""
     P, R = spec.P, spec.R
-    clean = _clean(spec)
+    clean = _clean(spec, snr_db)
     out = np.empty((batch, P, R), dtype)
     for b in range(batch):
         rng = np.random.Generator(np.random.PCG64(seed + b))
         w = (rng.standard_normal((P, R)) + 1j * rng.standard_normal((P, R))) * math.sqrt(0.5)
-        out[b] = clean + _clutter(spec, rng)[None, :] + w
+        x = clean + _clutter(spec, rng)[None, :] + w
+        out[b] = x * scale if scale != 1.0 else x
     return out
 
 

@@ -35,6 +35,14 @@ def oracle_flags(rdm, cfar_obj, near_tol=NEAR_TOL):
             np.stack([o[2] for o in out]))
 
 
+def oracle_flags_c(rdm, cfar_obj, near_tol=NEAR_TOL):
+    """oracle_flags from the C restatement (same rules, incl. the near-threshold mask;
+    cross-checked against the numpy oracle in test_oracle.py) for large shapes."""
+    c = oracle_cfar_dict(cfar_obj)
+    segs0 = list(cfar_obj.segments) or [(0, rdm.shape[-1])]
+    return coracle.cfar(rdm, c, segs0, near_tol=near_tol)
+
+
 def flag_mismatch(gpu, want, amb):
     """(hard mismatches outside the ambiguity band, mismatches inside it)."""
     diff = np.asarray(gpu) != np.asarray(want)

@@ -158,3 +158,44 @@ def test_dmx_mtd_pair_matches_generic_mtd():
     keep[nfft - m0:] = False
     np.testing.assert_allclose(s[keep], (ml + mr)[keep], rtol=0, atol=1e-9)
     assert not s[~keep].any() and keep.sum() == nfft - 2 * m0 - 1
+
+
+@pytest.mark.parametrize("rflag,methodV,methodR,refs", [(1, 0, 0, (5, 7)), (1, 1, 1, (3, 2)), (0, 0, 1, (8, 4)),
+                                                        (1, 1, 0, (8, 4))])
+def test_c_oracle_near_threshold_mask(rflag, methodV, methodR, refs):
+    """The C oracle's near-threshold mask (used at c4/c5 sizes) = the numpy oracle's
+    (rsp_ref.executeCFAR(near_tol)), with a tolerance wide enough to mark many cells."""
+    ref_n, guard = refs
+    rng = np.random.default_rng(11)
+    V, R = 96, 700
+    rdm = np.abs(rng.standard_normal((2, V, R)) + 1j * rng.standard_normal((2, V, R)))
+    rdm[:, 40, 100:103] = [9.0, 14.0, 13.9]
+    rdm[:, 60, 400] = 11.0
+    c = dict(refR=ref_n, saveR=guard, TR=2.5, methodR=methodR, refV=ref_n, saveV=guard, TV=2.5, methodV=methodV,
+             M0=3, rFlag=rflag, zero_v_div=20)
+    segs0 = [(0, 250), (250, 700)]
+    fc, fvc, ac = coracle.cfar(rdm, c, segs0, near_tol=0.05)
+    segs1 = [(a + 1, b) for a, b in segs0]
+    for i in range(2):
+        f, fv, a = ref.main_cfar_chain(rdm[i], c, segs1, 20, near_tol=0.05)
+        np.testing.assert_array_equal(fc[i], f)
+        np.testing.assert_array_equal(fvc[i], fv)
+        np.testing.assert_array_equal(ac[i], a)
+    assert ac.sum() > 50 and fc.sum() > 0
+
+
+def test_builtins_against_scipy():
+    """The oracle's restatements of MATLAB builtins against scipy's: filter(b, 1, x)
+    (scipy.signal.lfilter), hamming(n) (symmetric scipy window), kaiser(n, beta), and
+    round(mean(grpdelay(b))) (scipy.signal.group_delay of the 35-tap FIR)."""
+    sig = pytest.importorskip("scipy.signal")
+    rng = np.random.default_rng(5)
+    b = ref.FIR_TAPS_RAW / ref.FIR_TAPS_RAW.max()
+    x = rng.standard_normal(300) + 1j * rng.standard_normal(300)
+    np.testing.assert_allclose(ref.mfilter(b, x), sig.lfilter(b, [1.0], x), rtol=0, atol=1e-12)
+    for n in (2, 67, 1536, 2047):
+        np.testing.assert_allclose(ref.hamming(n), sig.windows.hamming(n, sym=True), rtol=0, atol=1e-14)
+        np.testing.assert_allclose(ref.kaiser(n, 8.0), sig.windows.kaiser(n, 8.0, sym=True), rtol=0, atol=1e-13)
+    _, gd = sig.group_delay((b, [1.0]), w=512)
+    assert abs(np.mean(gd) - 17.0) < 1e-6
+    assert ref.grpdelay_round_mean(b) == int(np.floor(np.mean(gd) + 0.5)) == 17
