@@ -63,7 +63,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--profile-every", type=int, default=7,
-                    help="bracket every N-th kernel launch with events (coprime with the 2-3 launches per chunk)")
+                    help="(unused; kept for old command lines)")
+    ap.add_argument("--lane-steps", type=int, default=2,
+                    help="steps of the single-lane per-kernel pass after the timed region (0 = skip)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.P = args.P or cfg["P"]
@@ -75,35 +77,91 @@ def parse():
     return args
 
 
+def host_cpus():
+    """The host's CPU facts for the baseline: nproc (os.cpu_count), the CPUs this process may
+    run on (sched_getaffinity), the cgroup CPU quota (cpu.max), the CPU model (lscpu), and the
+    thread count used = the smallest of affinity and quota (on the GPU box nproc shows the whole
+    machine, many times this job's share)."""
+    import math
+    import subprocess
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota_cpus"] = quota
+    try:
+        lscpu = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in lscpu.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)"):
+                info["lscpu_" + k.strip().lower().replace(" ", "_").replace("(s)", "s")] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    n = info["affinity"] or 1
+    if quota:
+        n = min(n, max(1, int(math.floor(quota))))
+    info["threads_used"] = n
+    return info
+
+
 def cpu_baseline(spec, cfar, seconds, unit="CPI/s"):
-    """fp64 C restatement (oracle/rsp_oracle.c, OpenMP over CPIs) on a bounded sample."""
+    """The CPU path beside the GPU: the fp64 C restatement of the MATLAB chain
+    (oracle/rsp_oracle.c, OpenMP over CPIs) timed on this host's CPU share and on one thread,
+    on a bounded sample of the same workload, plus the loop-faithful numpy oracle at c1
+    (64 x 1024, one CPI: the 'MATLAB-semantics' plumbing baseline)."""
     if seconds <= 0:
         return None
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import coracle
-    from rsp import synth
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = min(threads, 16)
-    pool_n = max(threads, 16)
+    import rsp_ref
+    from rsp import presets, synth
+    cpus = host_cpus()
+    threads = cpus["threads_used"]
+    pool_n = max(threads, 8)
     echo = synth.echo_numpy(spec, pool_n, seed=1003).astype(np.complex128)
     pre = coracle.preset(spec.name, spec.P, spec.R)
     c = cfar.as_dict() if cfar is not None else None
     if c is not None:
         c["zero_v_div"] = cfar.zero_v_div
-    done, t0 = 0, time.perf_counter()
-    while True:
-        rdm = coracle.pc_mtd(echo, pre, nthreads=threads)
-        if c is not None:
-            coracle.cfar(rdm, c, cfar.segments, nthreads=threads)
-        done += pool_n
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+
+    def run(nthreads, budget, n):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            rdm = coracle.pc_mtd(echo[:n], pre, nthreads=nthreads)
+            if c is not None:
+                coracle.cfar(rdm, c, cfar.segments, nthreads=nthreads)
+            done += n
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done, el
+
+    done, el = run(threads, 0.6 * seconds, pool_n)
+    done1, el1 = run(1, 0.3 * seconds, 1)
+    # c1: the numpy loop-faithful oracle, one 64 x 1024 CPI, fun_MTD_produce + main_cfar chain
+    s1 = presets.v2(64, 1024)
+    e1 = synth.echo_numpy(s1, 1, seed=1001)[0].astype(np.complex128)
+    c1 = presets.default_cfar(s1)
+    cd = c1.as_dict()
+    t1 = time.perf_counter()
+    m1 = rsp_ref.fun_MTD_produce_v2(e1, rsp_ref.v2_params(64, 1024))
+    rsp_ref.main_cfar_chain(m1, cd, [(a + 1, b) for a, b in c1.segments], c1.zero_v_div)
+    c1_s = time.perf_counter() - t1
     return {"value": done / el, "unit": unit, "cores": threads, "kind": "port",
-            "sample": "%d CPIs (%d x %d, %s preset%s) in %.1f s: a pool of %d distinct synthetic CPIs "
-                      "cycled; fp64 C restatement of the MATLAB chain (MATLAB itself is not available)"
-                      % (done, spec.P, spec.R, spec.name, " + CFAR" if c else "", el, pool_n)}
+            "sample": "%d CPIs (%d x %d, %s preset%s) in %.1f s on %d threads: a pool of %d distinct synthetic "
+                      "CPIs cycled; fp64 C restatement of the MATLAB chain with OpenMP over CPIs (MATLAB itself is "
+                      "not available)" % (done, spec.P, spec.R, spec.name, " + CFAR" if c else "", el, threads, pool_n),
+            "one_thread": {"value": done1 / el1, "unit": unit, "sample": "%d CPIs in %.1f s" % (done1, el1)},
+            "c1_numpy_oracle_s_per_cpi": round(c1_s, 3),
+            "host": cpus}
 
 
 def pmc_traffic(tag):
@@ -452,25 +510,12 @@ def main():
         if world > 1:
             dist.barrier()
 
-    launches_per_step = None
-    for i in range(args.warmup):
-        if i == 0 and not args.no_profile:
-            eng.profile(True, every=1)      # count launches per step (chunks) once, untimed
+    for _ in range(args.warmup):
         step()
-        if i == 0 and not args.no_profile:
-            launches_per_step = {k: n for k, (_, n) in eng.profile_read().items()}
-            eng.profile(False)
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # per-kernel device time, live: the library brackets every --profile-every-th launch of the
-    # timed steps with HIP events on the stream it is launched on (rsp_profile); read after
-    # the timed region.  Sampling keeps the events' own cost out of the measured throughput.
-    if not args.no_profile:
-        # a fused step is one or two launches: bracket each (the event pair is ~us of a ms step)
-        few = launches_per_step is not None and sum(launches_per_step.values()) <= 4
-        eng.profile(True, every=1 if few else args.profile_every)
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
@@ -484,10 +529,21 @@ def main():
     eng.chain_check()   # a fused launch whose bounded in-kernel wait expired invalidates the run
     elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, device=dev)
 
-    kernels = None
-    if not args.no_profile:
-        kernels = eng.profile_read()
+    # Per-kernel device times, measured separately from the throughput: a short pass on ONE
+    # chunk pipeline (rsp_set_streams(1)) with every launch bracketed by HIP events on the
+    # stream it runs on, so no two kernels overlap and each kernel's time per step is its own
+    # (in the timed region the two pipelines overlap PC of one chunk with MTD of the other).
+    kernels = launches = None
+    if not args.no_profile and args.lane_steps > 0 and not args.fused:
+        eng.set_streams(1)
+        eng.profile(True, every=1)
+        for _ in range(args.lane_steps):
+            step()
+        torch.cuda.synchronize(dev)
+        prof = eng.profile_read()
         eng.profile(False)
+        eng.set_streams(args.streams or 2)
+        kernels = {k: (ms / args.lane_steps, n // args.lane_steps) for k, (ms, n) in prof.items()}
 
     if rank == 0:
         esz = 4 if args.half else 8
@@ -501,39 +557,49 @@ def main():
         tag = "%s_P%d_R%d%s%s%s" % (args.preset, args.P, args.R, "" if cfar else "_nocfar",
                                     "_f16" if args.half else "", "_win%d" % win if win else "")
         pmc = pmc_traffic(tag)
-        # Dominant kernel (largest device time per step): achieved = §8d bytes per CPI x CPIs per
-        # launch / its mean launch duration (HIP events on its launch stream); traffic = HBM-side
-        # bytes per launch from the committed PMC summary.
-        roof = {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": None, "traffic": None, "alg_bytes_per_unit": cpi_bytes,
-                "chain": {"achieved": round(chain_gbps, 1), "frac": round(chain_gbps / HBM_PEAK_GBPS, 4),
-                          "note": "whole step: units/s x alg bytes per unit"}}
+        # Headline: the whole chain (SURVEY.md §8d algorithmic bytes per CPI x CPIs/s over one
+        # step, the dominant cost being two overlapping kernels); traffic = every kernel's
+        # PMC HBM-side bytes of a profiled run / the CPIs it processed.
+        roof = {"bound": "hbm", "kernel": "chain (PC + MTD/Doppler-CFAR + range CFAR, 2 pipelines)",
+                "achieved": round(chain_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(chain_gbps / HBM_PEAK_GBPS, 4), "traffic": None, "alg_bytes_per_unit": cpi_bytes,
+                "units_per_launch": units, "avg_launch_us": round(gpu_ms * 1e3 / args.steps, 1),
+                "note": "one step = one launch sequence over the batch; achieved = units/s (device events "
+                        "around the timed steps) x alg bytes per unit"}
+        if pmc and pmc.get("bytes_per_unit"):
+            roof["traffic"] = int(pmc["bytes_per_unit"])
+            roof["traffic_per"] = "unit (CPI or window), all kernels of a profiled run"
+            roof["traffic_ratio"] = round(pmc["bytes_per_unit"] / cpi_bytes, 3)
+            roof["traffic_source"] = "profiles/pmc_%s.json" % tag
         if kernels:
+            # each kernel's own compulsory bytes per launch: PC reads the echo and writes the
+            # pulse-compressed rows; MTD reads them and writes the RDM and the flag plane
+            npc = kernels.get("pc_kernel", (0, 0))[1]
+            pc_rows = (B + npc) * P * spec.beams if win else B * P * spec.beams
+            per_kernel_bytes = {
+                "pc_kernel": (pc_rows / max(npc, 1)) * (spec.R * esz + R * 8),
+                "mtd_kernel": units / max(kernels.get("mtd_kernel", (0, 1))[1], 1)
+                * (P * R * 8 * spec.beams + spec.V * R * 4 + (spec.V * R if cfar else 0)),
+            }
             ks = {}
             for name, (ms, n) in kernels.items():
-                avg_us = ms * 1e3 / n
-                ks[name] = {"avg_us": round(avg_us, 2), "sampled_launches": n,
-                            "launches_per_step": launches_per_step.get(name)}
-            dom = max(kernels, key=lambda k: kernels[k][0])
-            cpl = units / launches_per_step[dom]       # CPIs (windows) per launch
-            if dom == "pc_kernel" and win:
-                cpl = B / launches_per_step[dom] * win   # one PC launch serves its frames' windows
-            avg_s = kernels[dom][0] / 1e3 / kernels[dom][1]
-            ach = cpi_bytes * cpl / avg_s / 1e9
-            roof.update({"kernel": dom, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "units_per_launch": cpl, "alg_bytes_per_launch": int(cpi_bytes * cpl),
-                         "avg_launch_us": round(avg_s * 1e6, 2)})
-            if pmc and dom in pmc.get("kernels", {}):
-                kp = pmc["kernels"][dom]
-                scale = cpl / pmc["cpis_per_launch"] if pmc.get("cpis_per_launch") else 1.0
-                roof["traffic"] = int(kp["hbm_bytes_per_launch"] * scale)
-                roof["traffic_source"] = "profiles/pmc_%s.json" % tag
+                avg_us = ms * 1e3 / max(n, 1)
+                k = {"avg_us": round(avg_us, 2), "launches_per_step": n, "ms_per_step": round(ms, 3)}
+                if name in per_kernel_bytes:
+                    ab = per_kernel_bytes[name]
+                    k["alg_bytes_per_launch"] = int(ab)
+                    k["achieved"] = round(ab / (avg_us * 1e3), 1)
+                    k["frac"] = round(ab / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
+                if pmc and name in pmc.get("kernels", {}):
+                    k["hbm_bytes_per_launch"] = pmc["kernels"][name].get("hbm_bytes_per_launch")
+                ks[name] = k
             roof["kernels"] = ks
-            roof["kernel_sum_ms_per_step"] = round(
-                sum(kernels[k][0] / kernels[k][1] * launches_per_step[k] for k in kernels), 3)
-        else:
-            roof.update({"kernel": "chain", "achieved": round(chain_gbps, 1),
-                         "frac": round(chain_gbps / HBM_PEAK_GBPS, 4)})
+            roof["kernels_source"] = ("single-pipeline pass after the timed region (%d steps, every launch "
+                                      "bracketed by HIP events on its stream)" % args.lane_steps)
+            roof["kernel_sum_ms_per_step"] = round(sum(ms for ms, _ in kernels.values()), 3)
+            dom = max(kernels, key=lambda q: kernels[q][0])
+            roof["dominant_kernel"] = dom
+            roof["dominant_ms_per_step"] = round(kernels[dom][0], 3)
         achieved = chain_gbps
         cpu = None
         if world == 1:

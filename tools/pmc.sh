@@ -6,7 +6,7 @@ OUT="$ROOT/gpurun_out/pmc"
 rm -rf "$OUT"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="${BENCH_ARGS:---steps 2 --warmup 1}"
+ARGS="--steps ${PMC_STEPS:-2} --warmup 1 ${BENCH_ARGS:-}"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \

@@ -83,18 +83,22 @@ def main():
         for c, v in r.items():
             print("   %-22s %s" % (c, v))
     if "--json" in args:
-        # bench.py reads kernels[<name>].hbm_bytes_per_launch as roofline.traffic
+        # bench.py reads bytes_per_unit (roofline.traffic) and kernels[<name>].hbm_bytes_per_launch
         out = args[args.index("--json") + 1]
-        cpl = int(args[args.index("--cpis-per-launch") + 1]) if "--cpis-per-launch" in args else None
-        names = {}
-        doc = {"note": "rocprofv3 --pmc, one counter group per pass; HBM-side bytes per launch = "
-                       "2*FETCH_SIZE*1024 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM) + "
-                       "WRITE_SIZE*1024; Infinity-Cache hits are counted by these counters",
-               "cpis_per_launch": cpl, "kernels": {}}
+        units = float(args[args.index("--units-total") + 1]) if "--units-total" in args else None
+        doc = {"note": "rocprofv3 --pmc, one counter group per pass; HBM-side bytes = 2*FETCH_SIZE*1024 "
+                       "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM) + WRITE_SIZE*1024 per dispatch; "
+                       "Infinity-Cache hits are counted by these counters. bytes_per_unit = the bytes of every "
+                       "dispatch of the chain's kernels in the profiled run / the CPIs (windows) it processed",
+               "units_total": units, "kernels": {}}
+        total = 0.0
         for k, r in rows.items():
             r = dict(r)
             r["hbm_bytes_per_launch"] = int(round((r["read_MB"] + r["write_MB"]) * 1e6))
-            doc["kernels"][names.get(k, k)] = r
+            total += r["hbm_bytes_per_launch"] * r["dispatches"]
+            doc["kernels"][k] = r
+        if units:
+            doc["bytes_per_unit"] = round(total / units)
         json.dump(doc, open(out, "w"), indent=1)
 
 
