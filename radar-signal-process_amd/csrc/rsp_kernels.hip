@@ -266,13 +266,14 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     constexpr uint32_t ES = sizeof(TIn);
     const auto hr = buf_rsrc(a.mf.H, (uint32_t)N * 8u);
     float2 u[E];
+    const int e0 = t;   // the thread's element offset in each block of G
     constexpr int NW = tw_regs<N, E>() > 0 ? tw_regs<N, E>() : 1;
     float2 w[NW];
     tw_preload<N, G, 1, E, 0, NW>(w, t, tw);
     if constexpr (kUniform) {
         const auto xr = buf_rsrc(x + in_start, valid ? (uint32_t)in_len * ES : 0u);
 #pragma unroll
-        for (int m = 0; m < E; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
+        for (int m = 0; m < E; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)e0 * ES, (uint32_t)(G * m) * ES);
     } else {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
@@ -283,7 +284,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     float2 hs[kEarly ? E : 1];
     if constexpr (kEarly) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+        for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
     }
     if (a.do_fir) {
         if (valid)
@@ -301,7 +302,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         for (int m0 = 0; m0 < E; m0 += HB) {
             float2 h[HB];   // batches of spectrum loads, then the multiply
 #pragma unroll
-            for (int m = 0; m < HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * (m0 + m)) * 8u);
+            for (int m = 0; m < HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * (m0 + m)) * 8u);
 #pragma unroll
             for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
         }
@@ -310,7 +311,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
 #pragma unroll
-        for (int m = 0; m < E; ++m) buf_st_f2a<SA>(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+        for (int m = 0; m < E; ++m) buf_st_f2a<SA>(cconj(u[m]), yr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
     } else if (valid) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
@@ -353,104 +354,6 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_ker
     pc_row<TIn, N1, G>(echo, out, a1, b * PC::RPB1 + grp, t, lds + grp * PcCfg<N1>::SLOT);
 }
 
-// ---------------------------------------------------------------- persistent pair kernel
-// One long-segment row is G = T threads; the grid is sized to the resident block count and
-// each block walks the items blockIdx.x, +gridDim.x, ...: items [0, n2) are long-segment rows,
-// [n2, nitems) groups of RPB1 short-segment rows (FIR + MF).  Per long row: the row's
-// twiddles and its slice of H stay in registers for the whole launch, the next row's input
-// is loaded while this row runs the spectrum multiply and the inverse FFT, and the block
-// moves on without waiting for its stores -- the load, H-table and store-drain latencies
-// that bound the one-row-per-block kernel overlap with the FFT work.
-template <typename TIn, int N, int G>
-__device__ __forceinline__ void mf_load(float2 (&u)[N / G], const TIn* __restrict__ echo, const PcMfArgs& a,
-                                        int row, bool valid, int t) {
-    constexpr uint32_t ES = sizeof(TIn);
-    const auto xr = buf_rsrc(echo + (size_t)row * a.R + a.mf.in_start, valid ? (uint32_t)a.mf.in_len * ES : 0u);
-#pragma unroll
-    for (int m = 0; m < N / G; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)t * ES, (uint32_t)(G * m) * ES);
-}
-
-template <int N, int G>
-__device__ __forceinline__ void mf_store(const float2 (&u)[N / G], float2* __restrict__ out, const PcMfArgs& a,
-                                         int row, int t) {
-    const auto yr = buf_rsrc(out + (size_t)row * a.R_out + a.mf.out_start, (uint32_t)a.mf.out_len * 8u);
-#pragma unroll
-    for (int m = 0; m < N / G; ++m) buf_st_f2(cconj(u[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-}
-
-// The short-segment groups of a persistent PC workgroup: items first, +gridDim.x, ... < nitems.
-template <typename TIn, int N1, int N2>
-__device__ __forceinline__ void pc_short_items(const TIn* __restrict__ echo, float2* __restrict__ out,
-                                               const PcMfArgs& a1, int n2, int nitems, int first, float2* lds) {
-    using PC = PairCfg<N1, N2>;
-    constexpr int G1 = PcCfg<N1>::G;
-    const int grp = threadIdx.x / G1, t1 = threadIdx.x % G1;
-    // G1 == 64: a short row is one wave with its own LDS slot, so its exchanges need only the
-    // wave's own ordering: the four rows of a group no longer wait for each other at every
-    // FFT pass
-    constexpr bool WS = G1 == 64;
-    if constexpr (WS) __syncthreads();   // the long rows' last LDS reads are done
-    for (int item = first; item < nitems; item += (int)gridDim.x) {
-        if constexpr (!WS) __syncthreads();   // the previous item's last LDS reads are done
-        pc_row<TIn, N1, G1, 0, WS>(echo, out, a1, (item - n2) * PC::RPB1 + grp, t1, lds + grp * PcCfg<N1>::SLOT);
-    }
-}
-
-template <typename TIn, int N1, int N2>
-__global__ __launch_bounds__((PairCfg<N1, N2>::T), 2) void pc_persist_kernel(
-    const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int n2, int nitems) {
-    using PC = PairCfg<N1, N2>;
-    static_assert(PcCfg<N2>::G == PC::T, "one long-segment row per workgroup");
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    // Items blockIdx.x, +gridDim.x, ...: the long rows (< n2) come first in that sequence, then
-    // the short groups.  Short groups are latency-bound (FIR + two small FFTs per row, little
-    // VALU), so odd workgroups run theirs first: the two workgroups sharing a CU are out of
-    // phase, and one's latency overlaps the other's FFT work.
-    const int first_short = (int)blockIdx.x < n2
-                                ? (int)blockIdx.x + ((n2 - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x) *
-                                                        (int)gridDim.x
-                                : (int)blockIdx.x;
-    const bool shorts_first = blockIdx.x & 1;
-    if (shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
-    if ((int)blockIdx.x < n2) {
-        int item = blockIdx.x;
-        constexpr int G = PcCfg<N2>::G, E = N2 / G;
-        constexpr int NW = tw_regs<N2, E>() > 0 ? tw_regs<N2, E>() : 1;
-        const int t = threadIdx.x;
-        if (shorts_first) __syncthreads();   // the short items' last LDS reads are done
-        float2 w[NW];
-        tw_preload<N2, G, 1, E, 0, NW>(w, t, a2.mf.tw);
-        float2 h[E];
-        const auto hr = buf_rsrc(a2.mf.H, (uint32_t)N2 * 8u);
-#pragma unroll
-        for (int m = 0; m < E; ++m) h[m] = buf_ld_f2(hr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-        float2 u[E];
-        mf_load<TIn, N2, G>(u, echo, a2, item, true, t);
-        // settle the entry loads here, so the loop header carries no pending load (a merged
-        // wait state would put a vmcnt(0) -- a store drain -- at the top of every iteration)
-#pragma unroll
-        for (int m = 0; m < E; ++m) asm volatile("" ::"v"(u[m]), "v"(h[m]));
-        while (item < n2) {
-            const int next = item + (int)gridDim.x;
-            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, w);
-            float2 nx[E];   // next row in flight during the multiply + inverse FFT
-            mf_load<TIn, N2, G>(nx, echo, a2, next < n2 ? next : item, next < n2, t);
-#pragma unroll
-            for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], h[m]);   // conj(X.*H), 1/N in H
-            fft_reg_w<N2, G, 1, E, 0, NW>(u, lds, t, w);
-            // Consume the prefetch before the stores are issued: loads and stores share vmcnt
-            // on gfx9, so a wait placed after the stores (at the next row's first use) would
-            // also drain them.  Here the wait is for loads issued a multiply + IFFT ago.
-#pragma unroll
-            for (int m = 0; m < E; ++m) asm volatile("" ::"v"(nx[m]));
-            mf_store<N2, G>(u, out, a2, item, t);
-#pragma unroll
-            for (int m = 0; m < E; ++m) u[m] = nx[m];
-            item = next;
-        }
-    }
-    if (!shorts_first) pc_short_items<TIn, N1, N2>(echo, out, a1, n2, nitems, first_short, lds);
-}
 
 static int device_cus(int dev) {
     int cus = 0;
@@ -476,22 +379,6 @@ static hipError_t lds_attr(LaunchOnce& once, const void* kernel, size_t lds) {
     return launch_once(once, nullptr, [&](int, int*) {
         return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
-}
-
-template <typename TIn, int N1, int N2>
-static hipError_t launch_pc_persist(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs& a2,
-                                    hipStream_t s) {
-    using PC = PairCfg<N1, N2>;
-    static LaunchOnce once;
-    int resident = 0;
-    hipError_t e = resident_grid(once, (const void*)pc_persist_kernel<TIn, N1, N2>, PC::T, PC::lds, &resident);
-    if (e != hipSuccess) return e;
-    const int n2 = a1.rows;                                  // one item per long-segment row
-    const int nitems = n2 + (a1.rows + PC::RPB1 - 1) / PC::RPB1;
-    const int grid = nitems < resident ? nitems : resident;
-    hipLaunchKernelGGL((pc_persist_kernel<TIn, N1, N2>), dim3((unsigned)grid), dim3(PC::T), PC::lds, s, echo, out,
-                       a1, a2, n2, nitems);
-    return hipGetLastError();
 }
 
 bool pc_mf_supported(int nfft, int fir_stage_len) {
@@ -523,18 +410,14 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
 
 #define RSP_PAIR(n1, n2) \
     if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) return launch_pc_mf_n<TIn, n1, n2>(echo, out, a1, a2, s)
-#define RSP_PAIR_PERSIST(n1, n2)                                                              \
-    if (a1.mf.nfft == n1 && a2 && a2->mf.nfft == n2) {                                        \
-        return launch_pc_persist<TIn, n1, n2>(echo, out, a1, *a2, s);                         \
-    }
 
 template <typename TIn>
 static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a1, const PcMfArgs* a2,
                                  hipStream_t s) {
     // fused pairs of the built-in presets (v2 at 1024..16384 range bins, legacy)
     RSP_PAIR(1024, 1024);
-    RSP_PAIR_PERSIST(1024, 4096);
-    RSP_PAIR_PERSIST(1024, 8192);   // c4: PC 314 -> 185 us per launch against pc_mf_kernel
+    RSP_PAIR(1024, 4096);
+    RSP_PAIR(1024, 8192);
     RSP_PAIR(1024, 16384);
     RSP_PAIR(512, 1024);
     if (a2) return hipErrorNotSupported;
@@ -552,7 +435,6 @@ static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a
     }
 }
 #undef RSP_PAIR
-#undef RSP_PAIR_PERSIST
 
 bool pc_pair_supported(int n1, int n2) {
     return (n1 == 1024 && (n2 == 1024 || n2 == 4096 || n2 == 8192 || n2 == 16384)) || (n1 == 512 && n2 == 1024);
@@ -679,29 +561,48 @@ struct DopplerOut {
     bool zero_bg;                    // rflag: write the flag plane's zero background here
 };
 
-__device__ __forceinline__ void doppler_emit(const DopplerOut& o, bool hit, int i) {
-    const uint32_t so = (uint32_t)i * o.R;
-    if (o.want_fv) buf_st_u8(hit ? 1 : 0, o.fv, o.vo, so);
-    if (o.fused) {
-        if (!o.rflag) buf_st_u8(hit ? 1 : 0, o.fl, o.vo, so);   // flag = flagV (executeCFAR.m:91)
-        else {   // zero background (here, or pre-zeroed by the host); the range stage sets the detections
-            if (o.zero_bg) buf_st_u8(0, o.fl, o.vo, so);
-            const uint64_t bal = __ballot(hit);
-            if (bal) {   // rare: hits are sparse
-                const int lane = __lane_id();
-                const int leader = __builtin_ctzll(bal);
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(o.lds_count, (uint32_t)__popcll(bal));
-                base = __shfl(base, leader);
-                if (hit) st_u32_sc1(o.hits + base + __popcll(bal & ((1ull << lane) - 1)), o.cell0 + so);
-            }
-        }
+// The Doppler-stage outputs of a thread's run of N rows (bit i of `mask` = row v0+i is a hit):
+// flagV / flag bytes where requested (uniform branches, once per run), and the hits appended to
+// the workgroup's list.  Hits are sparse, so the append path is entered only by waves that
+// have one: one ballot over the masks, then per row one ballot and one LDS atomic per wave.
+template <int N>
+__device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t mask) {
+    if (o.want_fv) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) buf_st_u8((mask >> i) & 1u, o.fv, o.vo, (uint32_t)i * o.R);
+    }
+    if (!o.fused) return;
+    if (!o.rflag) {   // flag = flagV (executeCFAR.m:91)
+#pragma unroll
+        for (int i = 0; i < N; ++i) buf_st_u8((mask >> i) & 1u, o.fl, o.vo, (uint32_t)i * o.R);
+        return;
+    }
+    if (o.zero_bg) {   // zero background (here, or pre-zeroed); the range stage sets the detections
+#pragma unroll
+        for (int i = 0; i < N; ++i) buf_st_u8(0, o.fl, o.vo, (uint32_t)i * o.R);
+    }
+    if (__ballot(mask != 0u) == 0) return;   // the common case: no hit in the wave's rows
+    const int lane = __lane_id();
+    for (int i = 0; i < N; ++i) {
+        const bool hit = (mask >> i) & 1u;
+        const uint64_t bal = __ballot(hit);
+        if (!bal) continue;
+        const int leader = __builtin_ctzll(bal);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(o.lds_count, (uint32_t)__popcll(bal));
+        base = __shfl(base, leader);
+        if (hit) st_u32_sc1(o.hits + base + __popcll(bal & ((1ull << lane) - 1)), o.cell0 + (uint32_t)i * o.R);
     }
 }
 
+template <int N>
 __device__ __forceinline__ void doppler_flags(const float* mag, const float* sums, const CfarVArgs& cv, bool col_on,
                                               int v0, int v1, const DopplerOut& o) {
-    for (int v = v0; v < v1; ++v) doppler_emit(o, doppler_test(mag, sums, cv, col_on, v) != 0, v - v0);
+    uint32_t mask = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (v0 + i < v1 && doppler_test(mag, sums, cv, col_on, v0 + i)) mask |= 1u << i;
+    doppler_emit_mask<N>(o, mask);
 }
 
 // Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
@@ -733,6 +634,8 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
     const int kr = cv.hi - cv.save - 1 - REF - v0; // ... and a right window iff i <= kr
     const int b0 = cv.lo - v0, b1 = cv.hi - v0;    // tested rows: b0 <= i < b1
     const bool go = cv.method == 0;
+    static_assert(E <= 32, "row mask");
+    uint32_t mask = 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
         float sl = L[i], sr = Rw[i];
@@ -746,22 +649,23 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
         // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
         const float th = (go ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
         const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
-        doppler_emit(o, hit, i);
+        mask |= (hit ? 1u : 0u) << i;
     }
+    doppler_emit_mask<E>(o, mask);
 }
 
-// One wave evaluates the hits of region rg: REF/SAVE > 0 compile-time windows (every load of
-// a hit's window issues at once); 0: the runtime ref/save of CfarRArgs.
+// Threads first, first + step, ... evaluate the hits of region rg: REF/SAVE > 0 compile-time
+// windows (every load of a hit's window issues at once); 0: the runtime ref/save of CfarRArgs.
 template <int REF, int SAVE, int LA = 0>
 __device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, uint8_t* __restrict__ flag,
                                                 const uint32_t* __restrict__ hits,
                                                 const uint32_t* __restrict__ counts, int rg, int region,
-                                                const CfarRArgs& a, int lane) {
+                                                const CfarRArgs& a, int first, int step = 64) {
     const uint32_t n = ld_u32<LA>(counts + rg);
     const uint32_t* list = hits + (size_t)rg * region;
     const int R = a.R, V = a.V;
     const int ref = REF > 0 ? REF : a.ref, save = REF > 0 ? SAVE : a.save;
-    for (uint32_t i = lane; i < n; i += 64) {
+    for (uint32_t i = first; i < n; i += step) {
         const uint32_t idx = ld_u32<LA>(list + i);
         const uint32_t row = idx / (uint32_t)R;        // cpi * V + v
         const int r = (int)(idx - row * (uint32_t)R);
@@ -801,18 +705,20 @@ __device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, u
     }
 }
 
-// The previous chunk's range stage inside an MTD launch: the extra row of workgroups
-// (blockIdx.y == gridDim.y - 1), one wave per hit region.
-__device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (int)blockDim.x / 64;
+// The previous chunk's range stage inside an MTD launch: after its own tile, workgroup wg of
+// the launch's nwg evaluates the hit regions wg, wg + nwg, ... of the previous chunk on this
+// pipeline (the same tile shape, so normally exactly one), all its threads sharing a region's
+// hits -- the gathers' latency is spread over the whole launch instead of a serial loop in a
+// few dedicated workgroups.
+__device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nwg) {
     const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
-    for (int rg = blockIdx.x * nw + w; rg < a.prev_nregions; rg += gridDim.x * nw) {
+    for (int rg = wg; rg < a.prev_nregions; rg += nwg) {
         if (ref57)
             cfar_hit_region<5, 7>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
-                                  lane);
+                                  threadIdx.x, blockDim.x);
         else
             cfar_hit_region<0, 0>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
-                                  lane);
+                                  threadIdx.x, blockDim.x);
     }
 }
 
@@ -841,34 +747,12 @@ struct MtdTile {
 
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
-// The raw PC samples of one single-beam tile: lane (c, g) loads rows g + G*m of range bin c.
-template <int P, int LA, int E>
-__device__ __forceinline__ void mtd_tile_load(float2 (&v)[E], const float2* pc, int bx, const MtdArgs& a,
-                                              bool valid) {
-    using C = MtdCfg<P, 1>;
-    static_assert(E == C::E, "tile shape");
-    constexpr int G = C::G, W = C::W;
-    const int c = threadIdx.x % W, g = threadIdx.x / W;
-    const uint32_t R = (uint32_t)a.R_out;
-    const int r = bx * W + c;
-    const uint32_t vo_in = (valid && r < (int)R) ? ((uint32_t)g * R + (uint32_t)r) * 8u : kOob;
-    const auto src = buf_rsrc(pc, (uint32_t)a.pin * R * 8u);
-#pragma unroll
-    for (int m = 0; m < E; ++m) v[m] = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
-}
-
-// PRE: the tile's samples were loaded ahead (mtd_tile_load into `pre`, single beam).
-template <int P, int REF, int BEAMS, int LA, int SA, bool PRE = false>
-__device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem,
-                                         uint32_t* s_hits, const float2* pre = nullptr) {
+template <int P, int REF, int BEAMS, int LA, int SA>
+__device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem, uint32_t* s_hits) {
     using C = MtdCfg<P, BEAMS>;
     constexpr int G = C::G, E = C::E, W = C::W;
     if (threadIdx.x == 0) *s_hits = 0u;   // published by the FFT's barriers
-    // persistent use (PRE): an opaque copy of the thread index, so the tile's lane-derived
-    // addresses, window and twiddle loads are not hoisted out of the tile loop (and spilled)
-    int tx = threadIdx.x;
-    if constexpr (PRE) asm volatile("" : "+v"(tx));
-    const int c = tx % W, g = tx / W;
+    const int c = threadIdx.x % W, g = threadIdx.x / W;
     const uint32_t R = (uint32_t)a.R_out;
     const int r = T.bx * W + c;
     const bool rv = r < (int)R;
@@ -883,9 +767,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         const auto src = buf_rsrc(T.pc + (size_t)b * pin * R, (uint32_t)pin * R * 8u);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            float2 v;
-            if constexpr (PRE) v = pre[m];
-            else v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
+            const float2 v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
             const float w = a.win[g + G * m];
             u[m] = make_float2(v.x * w, v.y * w);
         }
@@ -971,7 +853,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
         doppler_sums(mag, sums, P, a.cv.ref, v0, v0 + E);
         __syncthreads();
-        doppler_flags(mag, sums, a.cv, col_on, v0, v0 + E, o);
+        doppler_flags<E>(mag, sums, a.cv, col_on, v0, v0 + E, o);
     }
     if (o.fused && o.rflag) {
         __syncthreads();
@@ -993,20 +875,15 @@ template <int P, int REF, int BEAMS>
 __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T)) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
-    const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
-    if (yoff && blockIdx.y == 0) {                  // dispatched first so it overlaps the tiles
-        prev_chunk_hits(a);
-        return;
-    }
     using C = MtdCfg<P, BEAMS>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_hits;
-    const size_t cpi = blockIdx.y - yoff;
+    const size_t cpi = blockIdx.y;
     const size_t R = (size_t)a.R_out;
     const size_t plane = (size_t)P * R;
     size_t row0 = cpi * (size_t)a.pin * BEAMS;                   // first PC row of this CPI
     if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)a.pin + a.win_start[cpi % a.nwin];
-    const uint32_t wg = (blockIdx.y - yoff) * gridDim.x + blockIdx.x;
+    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
     MtdTile T;
     T.pc = pc + row0 * R;
     T.rdm = rdm + cpi * plane;
@@ -1018,6 +895,7 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T)) void mtd_kernel(const float2
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
     mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
+    if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, (int)(gridDim.x * gridDim.y));
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
@@ -1031,18 +909,13 @@ template <int NF>
 __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const float2* __restrict__ pc,
                                                                float* __restrict__ rdm,
                                                                uint8_t* __restrict__ flagV, MtdArgs a) {
-    const int yoff = a.prev_nregions > 0 ? 1 : 0;   // row 0: the previous chunk's range stage,
-    if (yoff && blockIdx.y == 0) {                  // dispatched first so it overlaps the tiles
-        prev_chunk_hits(a);
-        return;
-    }
     using C = MtdCfg<NF>;
     constexpr int G = C::G, E = C::E, W = C::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_hits;
     if (threadIdx.x == 0) s_hits = 0u;
     const int c = threadIdx.x % W, g = threadIdx.x / W;
-    const size_t cpi = blockIdx.y - yoff;
+    const size_t cpi = blockIdx.y;
     const uint32_t R = (uint32_t)a.R_out;
     const int r = blockIdx.x * W + c;
     const bool rv = r < (int)R;
@@ -1076,7 +949,7 @@ __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const floa
         vr[m] = k < P ? v : -1;
         if (k < P) buf_st_f(x, dst, rv ? ((uint32_t)v * R + (uint32_t)r) * 4u : kOob, 0u);
     }
-    if (!a.cv.enabled) return;
+    if (!a.cv.enabled) return;   // (no CFAR: no range stage pending either)
     __syncthreads();  // the FFT exchange slots are free from here on
     float* mag = reinterpret_cast<float*>(smem) + c * C::MS;
 #pragma unroll
@@ -1094,18 +967,19 @@ __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const floa
     o.fl = buf_rsrc(o.fused ? a.flag + cpi * plane : nullptr, o.fused ? plane : 0u);
     o.vo = (rv && v0 < P) ? (uint32_t)v0 * R + (uint32_t)r : kOob;
     o.R = R;
-    const uint32_t wg = (blockIdx.y - yoff) * gridDim.x + blockIdx.x;
+    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
     o.hits = a.hits ? a.hits + (size_t)wg * ((size_t)W * P) : nullptr;
     o.lds_count = &s_hits;
     o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
     float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
     doppler_sums(mag, sums, P, a.cv.ref, v0, v1);
     __syncthreads();
-    doppler_flags(mag, sums, a.cv, col_on, v0, v1, o);
+    doppler_flags<E>(mag, sums, a.cv, col_on, v0, v1, o);
     if (o.fused && o.rflag) {
         __syncthreads();
         if (threadIdx.x == 0) a.hit_count[wg] = s_hits;
     }
+    if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, (int)(gridDim.x * gridDim.y));
 }
 
 template <int NF>
@@ -1118,7 +992,7 @@ static hipError_t launch_mtd_bluestein(const float2* pc, float* rdm, uint8_t* fl
     static LaunchOnce once;
     hipError_t e = lds_attr(once, (const void*)mtd_bluestein_kernel<NF>, C::lds);
     if (e != hipSuccess) return e;
-    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
+    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi),
         block(C::T);
     hipLaunchKernelGGL((mtd_bluestein_kernel<NF>), grid, block, C::lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
@@ -1138,7 +1012,7 @@ static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, in
     static LaunchOnce once;
     hipError_t e = lds_attr(once, (const void*)mtd_kernel<P, REF, BEAMS>, lds);
     if (e != hipSuccess) return e;
-    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)(ncpi + (a.prev_nregions > 0 ? 1 : 0))),
+    dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi),
         block(C::T);
     hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
