@@ -705,22 +705,93 @@ __device__ __forceinline__ void cfar_hit_region(const float* __restrict__ rdm, u
     }
 }
 
-// The previous chunk's range stage inside an MTD launch: after its own tile, workgroup wg of
-// the launch's nwg evaluates the hit regions wg, wg + nwg, ... of the previous chunk on this
-// pipeline (the same tile shape, so normally exactly one), all its threads sharing a region's
-// hits -- the gathers' latency is spread over the whole launch instead of a serial loop in a
-// few dedicated workgroups.
-__device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nwg) {
+// The previous chunk's range stage inside an MTD launch: workgroup wg of the launch's nwg
+// evaluates the hit regions wg, wg + nwg, ... of the previous chunk on this pipeline (the same
+// tile shape, so normally exactly one), all its threads sharing a region's hits.  `skip`: the
+// region-wg hits already done by a RangeJob.
+__device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nwg, int skip) {
     const bool ref57 = a.prev_cr.ref == 5 && a.prev_cr.save == 7;
     for (int rg = wg; rg < a.prev_nregions; rg += nwg) {
+        const int first = (int)threadIdx.x + (rg == wg ? skip : 0);
         if (ref57)
             cfar_hit_region<5, 7>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
-                                  threadIdx.x, blockDim.x);
+                                  first, blockDim.x);
         else
             cfar_hit_region<0, 0>(a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, rg, a.prev_region, a.prev_cr,
-                                  threadIdx.x, blockDim.x);
+                                  first, blockDim.x);
     }
 }
+
+// The range-stage share of one MTD workgroup for the reference's window (5 reference + 7 guard
+// cells, executeCFAR.m:45-84 with Function_CFAR1D_sub_fixCells.m:34-58): its region's first
+// blockDim hits, one per thread.  The hit count and the thread's hit index are loaded before
+// the tile, the 27 RDM cells r-13 .. r+13 of the hit's row right after the tile's own loads,
+// and the test + first-maximum scatter run after the tile -- the three dependent gathers hide
+// under the tile's FFT and Doppler CFAR instead of trailing the workgroup.
+struct RangeJob57 {
+    static constexpr int H = 13, NX = 2 * H + 1;
+    uint32_t n = 0, idx = 0;
+    float x[NX];
+    __device__ __forceinline__ void fetch_idx(const MtdArgs& a, int rg) {
+        // both loads issue at once: a region holds W*P >= blockDim entries, so the index load
+        // is in bounds (and ignored) past the count -- no count -> index round trip ahead of
+        // the tile's own loads
+        n = a.prev_count[rg];
+        idx = a.prev_hits[(size_t)rg * a.prev_region + threadIdx.x];
+    }
+    __device__ __forceinline__ void fetch_cells(const MtdArgs& a) {
+        const CfarRArgs& c = a.prev_cr;
+        const bool mine = threadIdx.x < n;
+        if (!__ballot(mine)) return;   // (wave-uniform) no hit in this wave
+        const uint32_t row = idx / (uint32_t)c.R;
+        const int r = (int)(idx - row * (uint32_t)c.R);
+        const int v = (int)(row % (uint32_t)c.V);
+        const bool zrow = v >= c.cz_lo && v < c.cz_hi;
+        const float* xr = a.prev_rdm + (size_t)row * c.R;
+        // branch-free: every lane of the wave loads (a clamped address), then selects; with no
+        // per-cell branch the loads stay here, ahead of the tile's FFT, and are waited on in finish()
+#pragma unroll
+        for (int k = 0; k < NX; ++k) {
+            const int q = r - H + k;
+            const bool ok = mine && !zrow && q >= 0 && q < c.R;
+            const float* p = ok ? xr + q : a.prev_rdm;
+            const float val = *p;
+            x[k] = ok ? val : 0.f;
+        }
+    }
+    __device__ __forceinline__ void finish(const MtdArgs& a) {
+        if (threadIdx.x >= n) return;
+        const CfarRArgs& c = a.prev_cr;
+        const uint32_t row = idx / (uint32_t)c.R;
+        const int r = (int)(idx - row * (uint32_t)c.R);
+        int slo, shi;
+        seg_of(r, c.nseg, c.seg_lo, c.seg_hi, slo, shi);
+        if (shi <= slo) return;
+        int best = -1;
+        float bx = 0.f;
+#pragma unroll
+        for (int e = -1; e <= 1; ++e) {
+            const int q = r + e, i = H + e;   // x[i] = cell q
+            float sl = 0.f, sr = 0.f;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                sl += x[i - 12 + k];
+                sr += x[i + 8 + k];
+            }
+            const bool lok = q - 12 >= slo, rok = q + 12 < shi;
+            const float xq = x[i];
+            if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, c.method, c.Tr) && (best < 0 || xq > bx)) {
+                best = q;
+                bx = xq;
+            }
+        }
+        if (best >= 0) a.prev_flag[(size_t)row * c.R + best] = 1;
+    }
+};
+
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
 
 // MTD: one workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the
 // tile, pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
@@ -747,8 +818,10 @@ struct MtdTile {
 
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
-template <int P, int REF, int BEAMS, int LA, int SA>
-__device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem, uint32_t* s_hits) {
+// after_loads(): called once the tile's first-beam loads are issued (RangeJob57 gathers).
+template <int P, int REF, int BEAMS, int LA, int SA, typename Hook = NoHook>
+__device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem, uint32_t* s_hits,
+                                         const Hook& after_loads = Hook()) {
     using C = MtdCfg<P, BEAMS>;
     constexpr int G = C::G, E = C::E, W = C::W;
     if (threadIdx.x == 0) *s_hits = 0u;   // published by the FFT's barriers
@@ -762,6 +835,12 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     const uint32_t vo_in = rv ? cell * 8u : kOob;
     float2 u[E];
     float m0[BEAMS == 2 ? E : 1];     // |X_0| while beam 1 runs
+    // the FFT's twiddles are loaded up front, with the tile: a twiddle load issued later (inside
+    // the FFT) would make every wait for it also wait for the after_loads() gathers (vmcnt
+    // counts in issue order)
+    constexpr int NW = tw_regs<P, E>() > 0 ? tw_regs<P, E>() : 1;
+    float2 tw[NW];
+    tw_preload<P, G, 1, E, 0, NW>(tw, g, a.tw);
 #pragma unroll
     for (int b = 0; b < BEAMS; ++b) {
         const auto src = buf_rsrc(T.pc + (size_t)b * pin * R, (uint32_t)pin * R * 8u);
@@ -771,7 +850,8 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             const float w = a.win[g + G * m];
             u[m] = make_float2(v.x * w, v.y * w);
         }
-        fft_reg<P, G, 1, E>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, a.tw);
+        if (b == 0) after_loads();
+        fft_reg_w<P, G, 1, E, 0, NW>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, tw);
         if constexpr (BEAMS == 2) {
             if (b == 0) {
 #pragma unroll
@@ -894,8 +974,18 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T)) void mtd_kernel(const float2
     T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
-    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
-    if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, (int)(gridDim.x * gridDim.y));
+    const int nwg = (int)(gridDim.x * gridDim.y);
+    const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions;
+    if (job) {
+        RangeJob57 rj;
+        rj.fetch_idx(a, (int)wg);
+        mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits, [&] { rj.fetch_cells(a); });
+        rj.finish(a);
+        if (rj.n > blockDim.x || a.prev_nregions > nwg) prev_chunk_hits(a, (int)wg, nwg, (int)blockDim.x);
+    } else {
+        mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
+        if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, nwg, 0);
+    }
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
@@ -979,7 +1069,7 @@ __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const floa
         __syncthreads();
         if (threadIdx.x == 0) a.hit_count[wg] = s_hits;
     }
-    if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, (int)(gridDim.x * gridDim.y));
+    if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, (int)(gridDim.x * gridDim.y), 0);
 }
 
 template <int NF>
