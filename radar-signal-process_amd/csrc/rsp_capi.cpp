@@ -12,6 +12,7 @@
 #include <complex>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -35,6 +36,7 @@ struct rsp_ctx {
     hipStream_t stream = nullptr;
     rsp::PcArgs pc{};
     bool pc_v2 = false;                 // per-segment specialised kernels (pc_mf_kernel)
+    bool pc_ols_off = false;            // RSP_PC_OLS=0 at create: no overlap-save split (A/B, tests)
     std::vector<rsp::PcMfArgs> pc_mf;   // one launch per matched-filter segment
     rsp::MtdArgs mtd{};
     int64_t V = 0;                      // Doppler rows (rsp_params.mtd_nfft or P)
@@ -171,6 +173,57 @@ static int twiddles(rsp_ctx* ctx, int n, const float2** out) {
     return RSP_OK;
 }
 
+// H = conj(FFT_n(scale * replica)) / n in fp64 (fft(x, n) truncates), and the n-point twiddles
+static int mf_spectrum(rsp_ctx* ctx, const rsp_pc_segment& g, int n, const float2** H, const float2** tw) {
+    std::vector<cd> a((size_t)n, cd(0, 0));
+    const int64_t L = g.coef_len < n ? g.coef_len : n;
+    for (int64_t k = 0; k < L; ++k) a[k] = g.scale * cd(g.coef_re[k], g.coef_im ? g.coef_im[k] : 0.0);
+    fft_pow2(a);
+    std::vector<float2> h((size_t)n);
+    for (int64_t k = 0; k < n; ++k) {
+        const cd v = std::conj(a[k]) / (double)n;
+        h[k] = make_float2((float)v.real(), (float)v.imag());
+    }
+    float2* dh = nullptr;
+    int rc = upload(ctx, h, &dh);
+    if (rc) return rc;
+    *H = dh;
+    return twiddles(ctx, n, tw);
+}
+
+// Overlap-save split of a long matched-filter segment (fun_lss_pulse_compression.m:64-72:
+// ifft(fft(x, nfft) .* conj(fft(h, nfft)))).  With nfft >= out_len + hlen - 1 no output of the
+// nfft-point circular correlation wraps, so output n = sum_k x[n + k] conj(h[k]) (x zero past
+// in_len) -- the same sums as nsub blocks of an nb-point correlation, block j producing outputs
+// [j*step, (j+1)*step), step = nb - hlen + 1.  A 16384-point row needs one 139 KB LDS slot
+// (one workgroup per CU, every phase exposed); nb = 4096 blocks run four workgroups per CU.
+// Kept only where it is exact in that sense and the FIR does not ride on the segment.
+static int pc_overlap_save(rsp_ctx* ctx, const rsp_pc_segment& g, rsp::PcMfArgs& a) {
+    a.nsub = 0;
+    a.sub_step = 0;
+    const int64_t nfft = a.mf.nfft;
+    const int64_t hlen = g.coef_len < nfft ? g.coef_len : nfft;
+    if (nfft <= 8192 || a.do_fir || nfft < (int64_t)a.mf.out_len + hlen - 1) return RSP_OK;
+    int best = 0, best_n = 0, best_step = 0;
+    for (int nb : {4096, 8192}) {
+        const int64_t step = nb - hlen + 1;
+        if (step < nb / 2) continue;
+        const int64_t n = (a.mf.out_len + step - 1) / step;
+        if (!best || n * nb < (int64_t)best_n * best) {
+            best = nb;
+            best_n = (int)n;
+            best_step = (int)step;
+        }
+    }
+    if (!best || (int64_t)best_n * best >= 2 * nfft) return RSP_OK;
+    int rc = mf_spectrum(ctx, g, best, &a.mf.H, &a.mf.tw);
+    if (rc) return rc;
+    a.mf.nfft = best;
+    a.nsub = best_n;
+    a.sub_step = best_step;
+    return RSP_OK;
+}
+
 static int ensure(rsp_ctx* ctx, DevBuf& b, size_t bytes) {
     if (b.n >= bytes && b.p) return RSP_OK;
     if (b.p) {
@@ -280,6 +333,7 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     rsp_ctx* ctx = new rsp_ctx();
     ctx->device = device;
     ctx->p = p;
+    if (const char* ols = std::getenv("RSP_PC_OLS")) ctx->pc_ols_off = std::atoi(ols) == 0;
     for (int s = 0; s < RSP_MAX_SEG; ++s) ctx->p.seg[s].coef_re = ctx->p.seg[s].coef_im = nullptr;
     auto bail = [&](int rc) {
         g_err = ctx->err;
@@ -354,22 +408,7 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
                 return bail(fail(ctx, RSP_ERR_ARG, "segment %d: in_len/out_len exceed nfft", s));
             d.nfft = (int)g.nfft;
             if (d.nfft > max_nfft) max_nfft = d.nfft;
-            // H = conj(FFT_nfft(scale * replica)) / nfft, in fp64 (fft(x, n) truncates)
-            std::vector<cd> a((size_t)g.nfft, cd(0, 0));
-            const int64_t L = g.coef_len < g.nfft ? g.coef_len : g.nfft;
-            for (int64_t k = 0; k < L; ++k)
-                a[k] = g.scale * cd(g.coef_re[k], g.coef_im ? g.coef_im[k] : 0.0);
-            fft_pow2(a);
-            std::vector<float2> h((size_t)g.nfft);
-            for (int64_t k = 0; k < g.nfft; ++k) {
-                const cd v = std::conj(a[k]) / (double)g.nfft;
-                h[k] = make_float2((float)v.real(), (float)v.imag());
-            }
-            float2* dh = nullptr;
-            int rc = upload(ctx, h, &dh);
-            if (rc) return bail(rc);
-            d.H = dh;
-            rc = twiddles(ctx, d.nfft, &d.tw);
+            int rc = mf_spectrum(ctx, g, d.nfft, &d.H, &d.tw);
             if (rc) return bail(rc);
         } else {
             return bail(fail(ctx, RSP_ERR_ARG, "segment %d: bad kind %d", s, g.kind));
@@ -418,6 +457,10 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
                 first = 0;
             } else if (!rsp::pc_mf_supported(a.mf.nfft, 0)) {
                 ok = false;
+            }
+            if (ok && !ctx->pc_ols_off) {
+                const int rc = pc_overlap_save(ctx, p.seg[s], a);
+                if (rc) return bail(rc);
             }
             ctx->pc_mf.push_back(a);
         }

@@ -68,6 +68,11 @@ struct PcMfArgs {
     int do_fir;
     SegDev fir;
     SegDev mf;
+    // overlap-save split of a long matched filter (nsub > 1): sub-block j of a row correlates
+    // input [in_start + j*sub_step, + mf.nfft) with the replica (mf.H, mf.nfft points) and keeps
+    // outputs [j*sub_step, (j+1)*sub_step) -- sub_step = mf.nfft - replica length + 1, so no
+    // output wraps.  nsub <= 1: the whole segment in one mf.nfft-point transform.
+    int nsub, sub_step;
     int nzero;
     int zero_lo[RSP_MAX_SEG + 1];
     int zero_hi[RSP_MAX_SEG + 1];

@@ -151,9 +151,10 @@ hipError_t launch_pc(const void* echo, int dtype, float2* out, int64_t rows, con
 // inverse FFT in registers, and the only LDS traffic is the inter-pass exchange.
 template <int N>
 struct PcCfg {
-    // 16 elements per thread; 32 from 16384 points on, so a row is 512 threads (2 waves per
-    // SIMD, a 256-VGPR budget) instead of 1024 (128 VGPRs: the preloaded twiddles spill)
-    static constexpr int G = N / (N >= 16384 ? 32 : 16);   // threads per row
+    // 16 elements per thread at every length: a 16384-point row is 1024 threads (4 waves per
+    // SIMD, 124 VGPRs with the lean twiddles) -- 32 elements at 512 threads took 164..174 VGPRs
+    // and left 2 waves per SIMD
+    static constexpr int G = N / 16;                       // threads per row
     static constexpr int E = N / G;                             // elements per thread
     static constexpr int RPB = G >= 256 ? 1 : 256 / G;          // rows per workgroup
     static constexpr int T = G * RPB;
@@ -248,7 +249,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
 // a wave, so the accesses stay per-lane predicated.
 template <typename TIn, int N, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
-                                       const PcMfArgs& a, int row, int t, float2* buf) {
+                                       const PcMfArgs& a, int row, int t, float2* buf, int sub = 0) {
     constexpr int E = N / G;
     constexpr bool kUniform = G % 64 == 0;
     // Short rows (G <= 64, the segment that also carries the FIR): every global load of the
@@ -260,8 +261,15 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     const bool valid = row < a.rows;
     const TIn* x = echo + (size_t)row * a.R;
     float2* y = out + (size_t)row * a.R_out;
-    const int in_start = a.mf.in_start, in_len = a.mf.in_len;
-    const int out_start = a.mf.out_start, out_len = a.mf.out_len;
+    int in_start = a.mf.in_start, in_len = a.mf.in_len;
+    int out_start = a.mf.out_start, out_len = a.mf.out_len;
+    if (a.nsub > 1) {   // overlap-save sub-block (wave-uniform): shifted input and output windows
+        const int off = sub * a.sub_step;
+        in_start += off;
+        out_start += off;
+        in_len = max(0, min(in_len - off, N));
+        out_len = max(0, min(out_len - off, a.sub_step));
+    }
     const float2* __restrict__ tw = a.mf.tw;
     constexpr uint32_t ES = sizeof(TIn);
     const auto hr = buf_rsrc(a.mf.H, (uint32_t)N * 8u);
@@ -301,13 +309,23 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #pragma unroll
         for (int m0 = 0; m0 < E; m0 += HB) {
             float2 h[HB];   // batches of spectrum loads, then the multiply
+#ifdef RSP_AB_NOH
+#pragma unroll
+            for (int m = 0; m < HB; ++m) h[m] = make_float2(a.mf.scale, 0.5f);
+#else
 #pragma unroll
             for (int m = 0; m < HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * (m0 + m)) * 8u);
+#endif
 #pragma unroll
             for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
         }
     }
+#ifndef RSP_AB_NOFFT2
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
+#endif
+#ifdef RSP_AB_NOSTORE
+    if (a.rows < 0)
+#endif
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
 #pragma unroll
@@ -340,18 +358,21 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_ker
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    // unit u of a segment = (row u / nsub, overlap-save sub-block u % nsub)
     if constexpr (N2 != 0) {
         if ((int)blockIdx.x < nblk2) {
             constexpr int G = PcCfg<N2>::G;
             const int grp = threadIdx.x / G, t = threadIdx.x % G;
-            pc_row<TIn, N2, G>(echo, out, a2, blockIdx.x * PC::RPB2 + grp, t, lds + grp * PcCfg<N2>::SLOT);
+            const int u = blockIdx.x * PC::RPB2 + grp, ns = a2.nsub > 1 ? a2.nsub : 1;
+            pc_row<TIn, N2, G>(echo, out, a2, u / ns, t, lds + grp * PcCfg<N2>::SLOT, u % ns);
             return;
         }
     }
     constexpr int G = PcCfg<N1>::G;
     const int grp = threadIdx.x / G, t = threadIdx.x % G;
     const int b = (int)blockIdx.x - (N2 ? nblk2 : 0);
-    pc_row<TIn, N1, G>(echo, out, a1, b * PC::RPB1 + grp, t, lds + grp * PcCfg<N1>::SLOT);
+    const int u = b * PC::RPB1 + grp, ns = a1.nsub > 1 ? a1.nsub : 1;   // (no FIR when ns > 1)
+    pc_row<TIn, N1, G>(echo, out, a1, u / ns, t, lds + grp * PcCfg<N1>::SLOT, u % ns);
 }
 
 
@@ -400,8 +421,14 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     static LaunchOnce once;
     hipError_t e = lds_attr(once, (const void*)pc_mf_kernel<TIn, N1, N2>, PC::lds);
     if (e != hipSuccess) return e;
-    const int nblk1 = (a1.rows + PC::RPB1 - 1) / PC::RPB1;
-    const int nblk2 = N2 ? (a1.rows + PC::RPB2 - 1) / PC::RPB2 : 0;
+#ifdef RSP_AB_NOSEG1
+    const int nblk1 = N2 ? 0 : (a1.rows + PC::RPB1 - 1) / PC::RPB1;
+#else
+    const int u1 = a1.rows * (a1.nsub > 1 ? a1.nsub : 1);
+    const int nblk1 = (u1 + PC::RPB1 - 1) / PC::RPB1;
+#endif
+    const int u2 = a2 ? a2->rows * (a2->nsub > 1 ? a2->nsub : 1) : 0;
+    const int nblk2 = N2 ? (u2 + PC::RPB2 - 1) / PC::RPB2 : 0;
     dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
     hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds, s, echo, out, a1,
                        a2 ? *a2 : a1, nblk2);
@@ -522,13 +549,17 @@ __device__ __forceinline__ void doppler_flags(const float* mag, const float* sum
 // runs register-resident with LDS exchanges, and |X| leaves in coalesced RDM rows.
 template <int P, int BEAMS = 1>
 struct MtdCfg {
-    // elements per thread: 32 from P = 512 on (one beam), so a tile keeps >= 16 range bins
-    // (>= 128-B row segments) as P grows; 16 below and for the two-beam pair (whose second
-    // beam's magnitudes already take E registers); 24 for the 3*2^k lengths
-    static constexpr int E = (P % 3 == 0) ? 24 : ((BEAMS == 1 && P >= 512) ? 32 : 16);
+    // elements per thread: 16 (24 for the 3*2^k lengths); from P = 512 on (one beam) the
+    // workgroup grows with G (512..1024 threads) so a tile keeps >= 8..16 range bins
+    // (>= 64..128-B row segments) and a thread still holds 16 elements -- E = 32 at 256 threads
+    // needed 169 VGPRs, 2 waves per SIMD
+    static constexpr int E = (P % 3 == 0) ? 24 : 16;
     static constexpr int G = P / E;                    // threads per range bin
     // threads per workgroup (512 for P = 256 measured neutral at c4: 529 vs 523 us per launch)
-    static constexpr int T = kBlock;
+    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024) : kBlock;
+    // minimum waves per SIMD (__launch_bounds__' second argument): two 512-thread workgroups
+    // per CU need <= 128 VGPRs
+    static constexpr int WPE = T == 512 ? 4 : 1;
     static constexpr int W = T / G;                    // range bins per workgroup
     static constexpr int SLOT = padded_len(P);         // FFT exchange slot (float2)
     static constexpr int MS = P + 1;                   // odd float stride of a CFAR column
@@ -952,7 +983,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 // the zero padding of fft(x, P, 1): out of the buffer's range, they load as 0).  BEAMS == 2:
 // the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
 template <int P, int REF, int BEAMS>
-__global__ __launch_bounds__((MtdCfg<P, BEAMS>::T)) void mtd_kernel(const float2* __restrict__ pc,
+__global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
     using C = MtdCfg<P, BEAMS>;
@@ -1872,7 +1903,7 @@ template <typename TIn>
 static hipError_t launch_chain_d(ChainArgs& a, hipStream_t s) {
     const bool ref5 = a.m.cv.enabled && a.m.cv.ref == 5;
     if constexpr (PairCfg<1024, 4096>::T == kBlock) {   // (a PC build with other row widths has no chain)
-        if (a.m.P == 128 && a.a1.mf.nfft == 1024 && a.a2.mf.nfft == 4096)
+        if (a.m.P == 128 && a.a1.mf.nfft == 1024 && a.a2.mf.nfft == 4096 && a.a1.nsub <= 1 && a.a2.nsub <= 1)
             return ref5 ? launch_chain_t<TIn, 1024, 4096, 128, 5>(a, s) : launch_chain_t<TIn, 1024, 4096, 128, 0>(a, s);
     }
     (void)ref5;

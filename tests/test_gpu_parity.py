@@ -33,7 +33,8 @@ def _echo(eng, batch, seed=1001):
 
 
 # ---------------------------------------------------------------- pulse compression alone
-@pytest.mark.parametrize("name,P,R", [("v2", 64, 1024), ("v2", 128, 4096), ("dmx", 64, 4096), ("legacy", 48, 1031)])
+@pytest.mark.parametrize("name,P,R", [("v2", 64, 1024), ("v2", 128, 4096), ("dmx", 64, 4096), ("legacy", 48, 1031),
+                                      ("v2", 16, 16384), ("v2", 16, 12000)])
 def test_pc_parity(torch_cuda, name, P, R):
     torch = torch_cuda
     eng = _engine(name, P, R)
@@ -60,6 +61,30 @@ def test_pc_parity(torch_cuda, name, P, R):
             want = ref.dmx_pulse_compression(e64[b], 0, R, H)
         err = np.linalg.norm(got[b] - want) / np.linalg.norm(want)
         assert err < RDM_TOL, (name, b, err)
+
+
+@pytest.mark.parametrize("R", [16384, 12000])
+def test_pc_overlap_save_matches_whole_transform(torch_cuda, monkeypatch, R):
+    """The 16384-point segment runs as overlap-save blocks of 4096 (pc_overlap_save); the
+    whole-length transform (RSP_PC_OLS=0) must give the same correlation to fp32 rounding,
+    and every column outside the split segment bit-identically."""
+    torch = torch_cuda
+    P = 16
+    outs = []
+    for ols in ("1", "0"):
+        monkeypatch.setenv("RSP_PC_OLS", ols)
+        eng = _engine("v2", P, R)
+        echo = _echo(eng, 1, seed=77)
+        d_in = torch.from_numpy(echo).cuda()
+        d_pc = torch.empty((1, P, R), dtype=torch.complex64, device="cuda")
+        eng.pc_dev(d_in, d_pc)
+        torch.cuda.synchronize()
+        outs.append(d_pc.cpu().numpy())
+        eng.close()
+    a, b = outs
+    assert np.array_equal(a[..., :951], b[..., :951])
+    err = np.linalg.norm(a - b) / np.linalg.norm(b)
+    assert err < 2e-6, err
 
 
 # ---------------------------------------------------------------- PC -> MTD -> 0-v
