@@ -556,7 +556,11 @@ struct MtdCfg {
     static constexpr int E = (P % 3 == 0) ? 24 : 16;
     static constexpr int G = P / E;                    // threads per range bin
     // threads per workgroup (512 for P = 256 measured neutral at c4: 529 vs 523 us per launch)
+#ifdef RSP_AB_MTDT
+    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? RSP_AB_MTDT : kBlock;
+#else
     static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024) : kBlock;
+#endif
     // minimum waves per SIMD (__launch_bounds__' second argument): two 512-thread workgroups
     // per CU need <= 128 VGPRs
     static constexpr int WPE = T == 512 ? 4 : 1;
@@ -589,6 +593,9 @@ struct DopplerOut {
     uint32_t* lds_count;             // workgroup hit counter (LDS)
     uint32_t cell0;                  // linear index of (v0, r) within the launch
     bool want_fv, fused, rflag;
+    bool coherent;                   // hit entries consumed inside this launch (fused chain):
+                                     // agent-scope stores; else plain stores (consumed by a
+                                     // later launch -- an sc1 store writes through the L2)
     bool zero_bg;                    // rflag: write the flag plane's zero background here
 };
 
@@ -613,16 +620,28 @@ __device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t 
         for (int i = 0; i < N; ++i) buf_st_u8(0, o.fl, o.vo, (uint32_t)i * o.R);
     }
     if (__ballot(mask != 0u) == 0) return;   // the common case: no hit in the wave's rows
+    // dense rows (the 0-v band edges fire in every column): one wave-wide prefix sum of the
+    // lanes' hit counts and one LDS atomic per wave, then each lane writes its run of entries
     const int lane = __lane_id();
+    const uint32_t cnt = (uint32_t)__popc(mask);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(o.lds_count, total);
+    base = __shfl(base, 0);
+    uint32_t* dst = o.hits + base + (incl - cnt);
+#pragma unroll
     for (int i = 0; i < N; ++i) {
-        const bool hit = (mask >> i) & 1u;
-        const uint64_t bal = __ballot(hit);
-        if (!bal) continue;
-        const int leader = __builtin_ctzll(bal);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(o.lds_count, (uint32_t)__popcll(bal));
-        base = __shfl(base, leader);
-        if (hit) st_u32_sc1(o.hits + base + __popcll(bal & ((1ull << lane) - 1)), o.cell0 + (uint32_t)i * o.R);
+        if ((mask >> i) & 1u) {
+            if (o.coherent) st_u32_sc1(dst, o.cell0 + (uint32_t)i * o.R);
+            else *dst = o.cell0 + (uint32_t)i * o.R;
+            ++dst;
+        }
     }
 }
 
@@ -682,6 +701,10 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
         const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
         mask |= (hit ? 1u : 0u) << i;
     }
+#ifdef RSP_AB_NOEMIT
+    if (o.vo == 0xfffffff0u) doppler_emit_mask<E>(o, mask);
+    return;
+#endif
     doppler_emit_mask<E>(o, mask);
 }
 
@@ -949,6 +972,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     DopplerOut o;
     o.want_fv = T.flagV != nullptr;
     o.fused = T.flag != nullptr;
+    o.coherent = SA != 0;
     o.rflag = a.rflag != 0;
     o.zero_bg = a.flag_zero != 0 && !bg_done;
     o.fv = buf_rsrc(o.want_fv ? T.flagV : nullptr, o.want_fv ? plane : 0u);
@@ -968,7 +992,10 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     }
     if (o.fused && o.rflag) {
         __syncthreads();
-        if (threadIdx.x == 0) st_u32_sc1(T.hit_count, *s_hits);
+        if (threadIdx.x == 0) {
+            if (SA != 0) st_u32_sc1(T.hit_count, *s_hits);
+            else *T.hit_count = *s_hits;
+        }
     }
 }
 
@@ -1006,6 +1033,9 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) voi
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
     const int nwg = (int)(gridDim.x * gridDim.y);
+#ifdef RSP_AB_NORJ
+    if (a.prev_nregions > 0) { mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits); return; }
+#endif
     const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions;
     if (job) {
         RangeJob57 rj;
@@ -1082,6 +1112,7 @@ __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const floa
     DopplerOut o;
     o.want_fv = flagV != nullptr;
     o.fused = a.flag != nullptr;
+    o.coherent = false;
     o.rflag = a.rflag != 0;
     o.zero_bg = a.flag_zero != 0;
     o.fv = buf_rsrc(o.want_fv ? flagV + cpi * plane : nullptr, o.want_fv ? plane : 0u);
@@ -1555,31 +1586,27 @@ __global__ __launch_bounds__(kBlock) void cfar_r16_kernel(const float* __restric
 // (Function_CFAR1D_sub_fixCells.m:34-58, one-sided fallback at segment edges); the first
 // maximum among passing candidates gets flag 1 (executeCFAR.m:64-84).  Several hits may
 // pick one cell; the writes are all 1.  Window sums are direct left-to-right adds.
-constexpr int kHitWaves = 4;   // regions per workgroup (one wave each)
-
-
-
+// One workgroup per region (a region is one MTD workgroup's hits: up to W*P entries, ~470
+// per region at c5, whose 0-v band edges fire in every column), its threads striding the list.
+constexpr int kHitThreads = 256;
 
 template <int REF, int SAVE>
-__global__ __launch_bounds__(64 * kHitWaves) void cfar_hits_kernel(const float* __restrict__ rdm,
-                                                                   uint8_t* __restrict__ flag,
-                                                                   const uint32_t* __restrict__ hits,
-                                                                   const uint32_t* __restrict__ counts, int nregions,
-                                                                   int region, CfarRArgs a) {
-    const int rg = blockIdx.x * kHitWaves + (int)(threadIdx.x >> 6);
-    if (rg >= nregions) return;
-    cfar_hit_region<REF, SAVE>(rdm, flag, hits, counts, rg, region, a, threadIdx.x & 63);
+__global__ __launch_bounds__(kHitThreads) void cfar_hits_kernel(const float* __restrict__ rdm,
+                                                                uint8_t* __restrict__ flag,
+                                                                const uint32_t* __restrict__ hits,
+                                                                const uint32_t* __restrict__ counts, int nregions,
+                                                                int region, CfarRArgs a) {
+    cfar_hit_region<REF, SAVE>(rdm, flag, hits, counts, (int)blockIdx.x, region, a, (int)threadIdx.x, kHitThreads);
 }
 
 hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
                             int nregions, int region, const CfarRArgs& a, hipStream_t s) {
     if (nregions <= 0) return hipSuccess;
-    const int grid = (nregions + kHitWaves - 1) / kHitWaves;
     if (a.ref == 5 && a.save == 7)   // the reference's parameters
-        hipLaunchKernelGGL((cfar_hits_kernel<5, 7>), dim3((unsigned)grid), dim3(64 * kHitWaves), 0, s, rdm, flag,
+        hipLaunchKernelGGL((cfar_hits_kernel<5, 7>), dim3((unsigned)nregions), dim3(kHitThreads), 0, s, rdm, flag,
                            hits, counts, nregions, region, a);
     else
-        hipLaunchKernelGGL((cfar_hits_kernel<0, 0>), dim3((unsigned)grid), dim3(64 * kHitWaves), 0, s, rdm, flag,
+        hipLaunchKernelGGL((cfar_hits_kernel<0, 0>), dim3((unsigned)nregions), dim3(kHitThreads), 0, s, rdm, flag,
                            hits, counts, nregions, region, a);
     return hipGetLastError();
 }
