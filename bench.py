@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-cfar", action="store_true", help="PC + MTD only")
     ap.add_argument("--half", action="store_true", help="fp16 I/Q input")
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--prefilter", action="store_true",
+                    help="fused iSTC (a synthetic stc curve) + MTI lag 30 in the chain (rsp_set_prefilter)")
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
     ap.add_argument("--fused", type=int, default=0, choices=[0, 1],
                     help="1: one-launch fused chain where the shape has one; 0: chunked pipeline (library default)")
@@ -482,6 +484,11 @@ def main():
     cfar = None if args.no_cfar else presets.default_cfar(spec)
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
     eng.set_fused(args.fused)
+    if args.prefilter:
+        import numpy as np
+        from rsp.prefilter import istc_gain
+        _, gain = istc_gain(np.linspace(-30.0, 0.0, 1025), spec.R)
+        eng.set_prefilter(gain=gain, mti_lag=30)
     B, P, R, win = args.batch, spec.P, spec.R_out, args.win
     units = B * win if win else B                   # CPIs (windows) per GPU per step
     # contiguous shard of the stream per rank (weak scaling): seed = 1000 + config id + first
@@ -634,6 +641,7 @@ def main():
             "config": {"workload": mode, "pulses": P, "range_bins": spec.R, "batch_per_gpu": B,
                        "windows_per_pair": win or None, "preset": args.preset,
                        "input": "c32f16" if args.half else "c64",
+                       "prefilter": "fused iSTC + MTI(30)" if args.prefilter else None,
                        "parallelism": "frame-sharded x%d, no collective" % world},
             "hbm_GBps_per_gpu": round(achieved, 1),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),

@@ -340,6 +340,17 @@ int rsp_motion_measure_dev(rsp_ctx* ctx, const float* d_sum, const float* d_diff
 int rsp_prefilter_dev(rsp_ctx* ctx, const void* d_in, void* d_out, int64_t P, int64_t R, int64_t batch,
                       const float* d_gain /* nullable, [R] */, int32_t mti_lag, void* stream);
 
+/* The same pre-filters fused into the context's chain (every rsp_pc_mtd*, rsp_run*, window
+ * entry point after this call), with no pass of their own over the echo:
+ *   gain != NULL (host, [R] linear gains as above): applied to each echo sample as pulse
+ *       compression loads it (needs the per-segment PC kernels -- the v2, dmx and legacy
+ *       presets; RSP_ERR_UNSUPPORTED otherwise);
+ *   mti_lag > 0: applied to the pulse-compressed rows as the MTD loads them -- pulse
+ *       compression is linear per row, so PC(x(m+lag) - x(m)) = PC(x(m+lag)) - PC(x(m)) --
+ *       over the pulses of each CPI (each window in window mode), zero for its last lag rows.
+ * gain == NULL and mti_lag == 0 switch the fused pre-filters off. */
+int rsp_set_prefilter(rsp_ctx* ctx, const float* gain /* nullable, host [R] */, int32_t mti_lag);
+
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1

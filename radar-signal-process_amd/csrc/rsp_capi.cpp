@@ -54,6 +54,7 @@ struct rsp_ctx {
     std::vector<void*> owned;           // constant tables (freed at destroy)
     std::map<int, float2*> tw;          // twiddle tables by length
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
+    DevBuf pf_gain;                     // fused iSTC gains (rsp_set_prefilter)
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
     DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
@@ -261,7 +262,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     if (!ctx) return RSP_OK;
     hipSetDevice(ctx->device);
     for (void* p : ctx->owned) hipFree(p);
-    DevBuf* bufs[] = {&ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
+    DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
                       &ctx->chain_ctl, &ctx->meas_band};
     for (DevBuf* b : bufs)
@@ -792,6 +793,27 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
     if (dtype != RSP_C64 && dtype != RSP_C32F16) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: dtype %d", dtype);
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
     HIP_TRY(ctx, run_pc(ctx, d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, (hipStream_t)stream));
+    return RSP_OK;
+}
+
+int rsp_set_prefilter(rsp_ctx* ctx, const float* gain, int32_t mti_lag) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_prefilter: null ctx");
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "rsp_set_prefilter: CFAR-only context");
+    if (mti_lag < 0) return fail(ctx, RSP_ERR_ARG, "rsp_set_prefilter: negative MTI lag %d", mti_lag);
+    if (gain && !ctx->pc_v2)
+        return fail(ctx, RSP_ERR_UNSUPPORTED, "rsp_set_prefilter: the fused gain needs the per-segment PC kernels");
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    HIP_TRY(ctx, hipDeviceSynchronize());   // no launch in flight still reads the old gains
+    const float* d_gain = nullptr;
+    if (gain) {
+        const size_t bytes = (size_t)ctx->p.R * sizeof(float);
+        const int rc = ensure(ctx, ctx->pf_gain, bytes);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipMemcpy(ctx->pf_gain.p, gain, bytes, hipMemcpyHostToDevice));
+        d_gain = (const float*)ctx->pf_gain.p;
+    }
+    for (rsp::PcMfArgs& a : ctx->pc_mf) a.gain = d_gain;
+    ctx->mtd.mti_lag = mti_lag;
     return RSP_OK;
 }
 

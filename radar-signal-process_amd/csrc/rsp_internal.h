@@ -73,6 +73,7 @@ struct PcMfArgs {
     // outputs [j*sub_step, (j+1)*sub_step) -- sub_step = mf.nfft - replica length + 1, so no
     // output wraps.  nsub <= 1: the whole segment in one mf.nfft-point transform.
     int nsub, sub_step;
+    const float* gain;   // fused iSTC (rsp_set_prefilter): echo column n scaled by gain[n], or null
     int nzero;
     int zero_lo[RSP_MAX_SEG + 1];
     int zero_hi[RSP_MAX_SEG + 1];
@@ -113,6 +114,7 @@ struct MtdArgs {
     int nwin;
     int win_start[RSP_MAX_WIN];
     int pin;             // pulses per CPI and beam (<= P; the FFT zero-pads rows pin..P-1)
+    int mti_lag;         // fused MTI (rsp_set_prefilter): pulse p reads row p+lag minus row p, 0 past pin-lag
     int beams;           // 2: DMX pair -- RDM = |X_0| + |X_1|, diff (if non-null) = |X_1| - |X_0|
     float* diff;
     // Bluestein plan for P without a radix plan (v2 native P = 332): bnf > 0 is the power-of-

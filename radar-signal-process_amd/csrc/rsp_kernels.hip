@@ -174,7 +174,8 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
 
 template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
-                                        const SegDev& g, float* stage, bool valid, int t) {
+                                        const SegDev& g, float* stage, bool valid, int t,
+                                        const float* __restrict__ gain) {
     float2* s2 = reinterpret_cast<float2*>(stage);
     const int kp = g.ntaps4 - 1;
     const int len = g.out_len;
@@ -185,6 +186,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
         // check), so the staging costs one memory round trip instead of one per element step.
         constexpr uint32_t ES = sizeof(TIn);
         const auto xr = buf_rsrc(x + g.in_start, valid ? (uint32_t)g.in_len * ES : 0u);
+        const auto gr = buf_rsrc(gain ? gain + g.in_start : nullptr, gain ? (uint32_t)g.in_len * 4u : 0u);
         constexpr int B = 8;
         for (int i0 = t; i0 < nst; i0 += B * G) {
             float2 v[B];
@@ -193,6 +195,13 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
                 const int j = i0 + q * G - kp;
                 v[q] = buf_ld_c((const TIn*)nullptr, xr, j >= 0 ? (uint32_t)j * ES : kOob, 0u);
             }
+            if (gain) {   // fused iSTC (wave-uniform)
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const int j = i0 + q * G - kp;
+                    v[q] = cscale(v[q], buf_ld_f(gr, j >= 0 ? (uint32_t)j * 4u : kOob, 0u));
+                }
+            }
 #pragma unroll
             for (int q = 0; q < B; ++q)
                 if (i0 + q * G < nst) s2[i0 + q * G] = v[q];
@@ -200,7 +209,9 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
     } else {
         for (int i = t; i < nst; i += G) {
             const int j = i - kp;
-            s2[i] = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+            float2 v = (valid && j >= 0 && j < g.in_len) ? ld_c(x + g.in_start + j) : make_float2(0.f, 0.f);
+            if (gain && j >= 0 && j < g.in_len) v = cscale(v, gain[g.in_start + j]);
+            s2[i] = v;
         }
     }
     xsync<WS>();
@@ -257,7 +268,10 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     // round trip overlaps the FIR instead of three in sequence.  Long rows keep the spectrum
     // loads after the forward FFT (32 fewer live VGPRs across it).
     constexpr bool kEarly = G <= 64;
-    if constexpr (kUniform) row = __builtin_amdgcn_readfirstlane(row);
+    if constexpr (kUniform) {   // (a VGPR-held offset in a buffer resource means a waterfall loop per access)
+        row = __builtin_amdgcn_readfirstlane(row);
+        sub = __builtin_amdgcn_readfirstlane(sub);
+    }
     const bool valid = row < a.rows;
     const TIn* x = echo + (size_t)row * a.R;
     float2* y = out + (size_t)row * a.R_out;
@@ -269,6 +283,12 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         out_start += off;
         in_len = max(0, min(in_len - off, N));
         out_len = max(0, min(out_len - off, a.sub_step));
+        if constexpr (kUniform) {
+            in_len = __builtin_amdgcn_readfirstlane(in_len);
+            out_len = __builtin_amdgcn_readfirstlane(out_len);
+            in_start = __builtin_amdgcn_readfirstlane(in_start);
+            out_start = __builtin_amdgcn_readfirstlane(out_start);
+        }
     }
     const float2* __restrict__ tw = a.mf.tw;
     constexpr uint32_t ES = sizeof(TIn);
@@ -289,6 +309,11 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
         }
     }
+    if (a.gain) {   // fused iSTC (rsp_set_prefilter): echo column n times gain[n]
+        const auto gr = buf_rsrc(a.gain + in_start, (uint32_t)in_len * 4u);
+#pragma unroll
+        for (int m = 0; m < E; ++m) u[m] = cscale(u[m], buf_ld_f(gr, (uint32_t)e0 * 4u, (uint32_t)(G * m) * 4u));
+    }
     float2 hs[kEarly ? E : 1];
     if constexpr (kEarly) {
 #pragma unroll
@@ -298,7 +323,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
                 for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) st_c<SA>(y + c, make_float2(0.f, 0.f));
-        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t);
+        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t, a.gain);
     }
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
     if constexpr (kEarly) {
@@ -898,11 +923,22 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 #pragma unroll
     for (int b = 0; b < BEAMS; ++b) {
         const auto src = buf_rsrc(T.pc + (size_t)b * pin * R, (uint32_t)pin * R * 8u);
+        if (a.mti_lag > 0) {   // fused MTI (wave-uniform): pulse p = PC(p + lag) - PC(p), 0 past pin - lag
+            const int lag = a.mti_lag;
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const float2 v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
-            const float w = a.win[g + G * m];
-            u[m] = make_float2(v.x * w, v.y * w);
+            for (int m = 0; m < E; ++m) {
+                const float2 v0 = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
+                const float2 v1 = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m + lag) * R * 8u);
+                const float w = g + G * m + lag < pin ? a.win[g + G * m] : 0.f;
+                u[m] = make_float2((v1.x - v0.x) * w, (v1.y - v0.y) * w);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const float2 v = buf_ld_f2a<LA>(src, vo_in, (uint32_t)(G * m) * R * 8u);
+                const float w = a.win[g + G * m];
+                u[m] = make_float2(v.x * w, v.y * w);
+            }
         }
         if (b == 0) after_loads();
         fft_reg_w<P, G, 1, E, 0, NW>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, tw);
@@ -1077,9 +1113,20 @@ __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const floa
     const auto src = buf_rsrc(pc + row0 * R, plane * 8u);           // rows >= P load as 0
     const uint32_t vo_in = rv ? ((uint32_t)g * R + (uint32_t)r) * 8u : kOob;
     float2 u[E];
+    if (a.mti_lag > 0) {   // fused MTI, as mtd_tile
+        const int lag = a.mti_lag;
 #pragma unroll
-    for (int m = 0; m < E; ++m)
-        u[m] = cmul(buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u), a.bwc[g + G * m]);
+        for (int m = 0; m < E; ++m) {
+            const float2 v0 = buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u);
+            const float2 v1 = buf_ld_f2(src, vo_in, (uint32_t)(G * m + lag) * R * 8u);
+            const float2 d = g + G * m + lag < P ? make_float2(v1.x - v0.x, v1.y - v0.y) : make_float2(0.f, 0.f);
+            u[m] = cmul(d, a.bwc[g + G * m]);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < E; ++m)
+            u[m] = cmul(buf_ld_f2(src, vo_in, (uint32_t)(G * m) * R * 8u), a.bwc[g + G * m]);
+    }
     float2* slot = reinterpret_cast<float2*>(smem) + c * C::SLOT;
     fft_reg<NF, G, 1, E>(u, slot, g, a.tw);
 #pragma unroll

@@ -30,7 +30,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check", "rsp_ingest_record_bytes",
-           "rsp_ingest_ddc_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev")
+           "rsp_ingest_ddc_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter")
 RSP_NKERNELS = 5
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "chain_kernel")
 
@@ -135,6 +135,8 @@ def load_library(path=None):
     lib.rsp_set_streams.argtypes = [vp, i32]
     lib.rsp_set_fused.restype = C.c_int
     lib.rsp_set_fused.argtypes = [vp, i32]
+    lib.rsp_set_prefilter.restype = C.c_int
+    lib.rsp_set_prefilter.argtypes = [vp, C.POINTER(C.c_float), i32]
     lib.rsp_chain_check.restype = C.c_int
     lib.rsp_chain_check.argtypes = [vp]
     lib.rsp_ingest_record_bytes.restype = C.c_int

@@ -63,6 +63,18 @@ class Engine:
         """One-launch fused chain where the shape has one (1); 0 = chunked pipeline (default)."""
         capi.check(self.lib.rsp_set_fused(self.ctx, int(enable)), self.ctx)
 
+    def set_prefilter(self, gain=None, mti_lag=0):
+        """Fuse iSTC (gain: [R] linear gains, e.g. rsp.prefilter.istc_gain) into pulse
+        compression's echo load and MTI (lag, e.g. 30) into the MTD's load of the PC rows
+        (rsp_set_prefilter); gain=None and mti_lag=0 switch them off."""
+        g = None
+        if gain is not None:
+            g = np.ascontiguousarray(gain, dtype=np.float32)
+            if g.shape != (self.spec.R,):
+                raise ValueError("gain must have R = %d entries" % self.spec.R)
+        ptr = g.ctypes.data_as(C.POINTER(C.c_float)) if g is not None else None
+        capi.check(self.lib.rsp_set_prefilter(self.ctx, ptr, int(mti_lag)), self.ctx)
+
     def chain_check(self):
         """Raise if a fused launch of this context gave up waiting for an item."""
         capi.check(self.lib.rsp_chain_check(self.ctx), self.ctx)
