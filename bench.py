@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-cfar", action="store_true", help="PC + MTD only")
     ap.add_argument("--half", action="store_true", help="fp16 I/Q input")
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time the PCIe-inclusive host entry point (rsp_pc_mtd_cfar, C128 column-major "
+                         "host echo as MATLAB holds it, RDM + flags back to host)")
     ap.add_argument("--prefilter", action="store_true",
                     help="fused iSTC (a synthetic stc curve) + MTI lag 30 in the chain (rsp_set_prefilter)")
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
@@ -112,6 +115,28 @@ def host_cpus():
         n = min(n, max(1, int(math.floor(quota))))
     info["threads_used"] = n
     return info
+
+
+def host_path(eng, echo, cfar, args, n=32, reps=3):
+    """The MEX-style host entry point: rsp_pc_mtd_cfar on a host complex128 echo in MATLAB's
+    column-major layout ([b][R][P] C order), RDM and flags returned to host column-major -- H2D
+    of 16 B per sample, the chain, D2H of 6 B per cell, and the layout/precision conversions
+    on the GPU.  Secondary figure; never the headline value."""
+    import numpy as np
+    from rsp import _capi as capi
+    if echo.dtype != __import__("torch").complex64:
+        return None
+    n = min(n, echo.shape[0])
+    h = np.ascontiguousarray(np.swapaxes(echo[:n].cpu().numpy().astype(np.complex128), 1, 2))
+    eng.pc_mtd_cfar(h, cfar, layout=capi.RSP_COLMAJOR, out_layout=capi.RSP_COLMAJOR)   # warm-up
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.pc_mtd_cfar(h, cfar, layout=capi.RSP_COLMAJOR, out_layout=capi.RSP_COLMAJOR)
+    el = time.perf_counter() - t0
+    return {"value": round(n * reps / el, 1), "unit": "CPI/s", "cpis_per_call": n, "calls": reps,
+            "input": "host C128 column-major (MATLAB layout)", "output": "host f32 RDM + u8 flag/flagV, column-major",
+            "bytes_per_cpi_pcie": int(eng.spec.P * eng.spec.R * 16 + eng.spec.V * eng.spec.R_out * 6),
+            "note": "PCIe-inclusive synchronous host API (rsp_pc_mtd_cfar); pageable numpy buffers"}
 
 
 def cpu_baseline(spec, cfar, seconds, unit="CPI/s"):
@@ -608,6 +633,7 @@ def main():
             roof["dominant_kernel"] = dom
             roof["dominant_ms_per_step"] = round(kernels[dom][0], 3)
         achieved = chain_gbps
+        host = host_path(eng, echo, cfar, args) if (args.host_path and world == 1 and not win) else None
         cpu = None
         if world == 1:
             # window mode: the reference runs fun_MTD_produce per window, so its rate is CPIs/s
@@ -648,6 +674,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if host is not None:
+            out["host_path"] = host
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -161,6 +161,15 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* params);
  * circshift, kaiser(P, 8) + fftshift MTD and fun_0v_pressing /150. */
 int rsp_create_v2(rsp_ctx** out, int device, int64_t P, int64_t R, const int64_t point_prt[4],
                   double fs, double B, const double tao[3]);
+/* Context for the legacy one-argument MTD_Signal = fun_MTD_produce(echo)
+ * (MatlabProcess_xuzerui/fun_MTD_produce.m:3-126; called at main_produce_dataset_win_xzr.m:37-38):
+ * P = prtNum, R = echo width, the hard-coded split 82 / 242 / R-324 (:24-38), the 35-tap FIR
+ * /max /1.2 with no group-delay shift, the two measured pulses the .m file holds inline
+ * (pulse2: n2 samples, pulse3: n3 samples, as separate real / imaginary arrays -- the shim
+ * reads them from the repository's data files), kaiser(P, 8) + fftshift MTD, 0-v /150. */
+int rsp_create_legacy(rsp_ctx** out, int device, int64_t P, int64_t R, const double* pulse2_re,
+                      const double* pulse2_im, int64_t n2, const double* pulse3_re, const double* pulse3_im,
+                      int64_t n3);
 int rsp_destroy(rsp_ctx* ctx);
 const char* rsp_last_error(const rsp_ctx* ctx);
 

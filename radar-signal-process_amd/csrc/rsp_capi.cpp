@@ -599,6 +599,52 @@ int rsp_create_v2(rsp_ctx** out, int device, int64_t P, int64_t R, const int64_t
     return rsp_create(out, device, &prm);
 }
 
+int rsp_create_legacy(rsp_ctx** out, int device, int64_t P, int64_t R, const double* pulse2_re,
+                      const double* pulse2_im, int64_t n2, const double* pulse3_re, const double* pulse3_im,
+                      int64_t n3) {
+    if (!out || !pulse2_re || !pulse2_im || !pulse3_re || !pulse3_im || n2 < 1 || n3 < 1)
+        return fail(nullptr, RSP_ERR_ARG, "rsp_create_legacy: bad argument");
+    const int64_t p1 = 82, p2 = 242, p3 = R - 324;   // fun_MTD_produce.m:24-38 (legacy)
+    if (p3 < 1) return fail(nullptr, RSP_ERR_SHAPE, "rsp_create_legacy: R=%lld <= 324", (long long)R);
+    std::vector<double> taps(35);
+    for (int i = 0; i < 35; ++i) taps[i] = kFirTaps[i] / 511.0;   // filter_coef / max
+    rsp_params prm;
+    std::memset(&prm, 0, sizeof(prm));
+    prm.P = P;
+    prm.R = R;
+    prm.R_out = R;
+    prm.nseg = 3;
+    prm.window = RSP_WIN_KAISER;
+    prm.window_beta = 8.0;
+    prm.fftshift = 1;
+    prm.zero_v_div = 150;
+    rsp_pc_segment& a = prm.seg[0];
+    a.kind = RSP_SEG_FIR;
+    a.fir_shift = 0;    // the legacy version keeps the FIR's group delay
+    a.in_start = 0;
+    a.in_len = a.out_len = p1;
+    a.scale = 1.0 / 1.2;
+    a.coef_len = 35;
+    a.coef_re = taps.data();
+    const double* re[2] = {pulse2_re, pulse3_re};
+    const double* im[2] = {pulse2_im, pulse3_im};
+    const int64_t n[2] = {n2, n3};
+    const int64_t m3 = R - p1 - p2;
+    for (int k = 0; k < 2; ++k) {
+        rsp_pc_segment& g = prm.seg[k + 1];
+        g.kind = RSP_SEG_MF;
+        g.in_start = g.out_start = k == 0 ? p1 : p1 + p2;
+        g.in_len = k == 0 ? p2 : m3;
+        g.out_len = k == 0 ? p2 : p3;
+        g.coef_len = n[k];
+        g.nfft = nextpow2(g.in_len + g.coef_len - 1);
+        g.scale = 1.0;
+        g.coef_re = re[k];
+        g.coef_im = im[k];
+    }
+    return rsp_create(out, device, &prm);
+}
+
 int rsp_set_streams(rsp_ctx* ctx, int32_t n) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_streams: null ctx");
     if (n < 1 || n > 4) return fail(ctx, RSP_ERR_ARG, "rsp_set_streams: n must be 1..4");

@@ -28,7 +28,7 @@ RSP_WIN_KAISER, RSP_WIN_HAMMING, RSP_WIN_RECT = 0, 1, 2
 EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_set_chunk",
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
-           "rsp_create_v2", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
+           "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_fused", "rsp_chain_check", "rsp_ingest_record_bytes",
            "rsp_ingest_ddc_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter")
 RSP_NKERNELS = 5
@@ -131,6 +131,9 @@ def load_library(path=None):
     lib.rsp_create_v2.restype = C.c_int
     lib.rsp_create_v2.argtypes = [C.POINTER(vp), C.c_int, i64, i64, C.POINTER(i64), C.c_double, C.c_double,
                                   C.POINTER(C.c_double)]
+    dp = C.POINTER(C.c_double)
+    lib.rsp_create_legacy.restype = C.c_int
+    lib.rsp_create_legacy.argtypes = [C.POINTER(vp), C.c_int, i64, i64, dp, dp, i64, dp, dp, i64]
     lib.rsp_set_streams.restype = C.c_int
     lib.rsp_set_streams.argtypes = [vp, i32]
     lib.rsp_set_fused.restype = C.c_int
