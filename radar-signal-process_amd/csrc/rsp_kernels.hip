@@ -334,23 +334,13 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #pragma unroll
         for (int m0 = 0; m0 < E; m0 += HB) {
             float2 h[HB];   // batches of spectrum loads, then the multiply
-#ifdef RSP_AB_NOH
-#pragma unroll
-            for (int m = 0; m < HB; ++m) h[m] = make_float2(a.mf.scale, 0.5f);
-#else
 #pragma unroll
             for (int m = 0; m < HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * (m0 + m)) * 8u);
-#endif
 #pragma unroll
             for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
         }
     }
-#ifndef RSP_AB_NOFFT2
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
-#endif
-#ifdef RSP_AB_NOSTORE
-    if (a.rows < 0)
-#endif
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
 #pragma unroll
@@ -446,12 +436,8 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     static LaunchOnce once;
     hipError_t e = lds_attr(once, (const void*)pc_mf_kernel<TIn, N1, N2>, PC::lds);
     if (e != hipSuccess) return e;
-#ifdef RSP_AB_NOSEG1
-    const int nblk1 = N2 ? 0 : (a1.rows + PC::RPB1 - 1) / PC::RPB1;
-#else
     const int u1 = a1.rows * (a1.nsub > 1 ? a1.nsub : 1);
     const int nblk1 = (u1 + PC::RPB1 - 1) / PC::RPB1;
-#endif
     const int u2 = a2 ? a2->rows * (a2->nsub > 1 ? a2->nsub : 1) : 0;
     const int nblk2 = N2 ? (u2 + PC::RPB2 - 1) / PC::RPB2 : 0;
     dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
@@ -581,11 +567,7 @@ struct MtdCfg {
     static constexpr int E = (P % 3 == 0) ? 24 : 16;
     static constexpr int G = P / E;                    // threads per range bin
     // threads per workgroup (512 for P = 256 measured neutral at c4: 529 vs 523 us per launch)
-#ifdef RSP_AB_MTDT
-    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? RSP_AB_MTDT : kBlock;
-#else
     static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024) : kBlock;
-#endif
     // minimum waves per SIMD (__launch_bounds__' second argument): two 512-thread workgroups
     // per CU need <= 128 VGPRs
     static constexpr int WPE = T == 512 ? 4 : 1;
@@ -726,10 +708,6 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
         const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
         mask |= (hit ? 1u : 0u) << i;
     }
-#ifdef RSP_AB_NOEMIT
-    if (o.vo == 0xfffffff0u) doppler_emit_mask<E>(o, mask);
-    return;
-#endif
     doppler_emit_mask<E>(o, mask);
 }
 
@@ -1069,9 +1047,6 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) voi
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
     const int nwg = (int)(gridDim.x * gridDim.y);
-#ifdef RSP_AB_NORJ
-    if (a.prev_nregions > 0) { mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits); return; }
-#endif
     const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions;
     if (job) {
         RangeJob57 rj;
