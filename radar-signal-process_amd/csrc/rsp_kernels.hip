@@ -379,7 +379,7 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_ker
             constexpr int G = PcCfg<N2>::G;
             const int grp = threadIdx.x / G, t = threadIdx.x % G;
             const int u = blockIdx.x * PC::RPB2 + grp, ns = a2.nsub > 1 ? a2.nsub : 1;
-            pc_row<TIn, N2, G>(echo, out, a2, u / ns, t, lds + grp * PcCfg<N2>::SLOT, u % ns);
+            pc_row<TIn, N2, G, 0, G == 64>(echo, out, a2, u / ns, t, lds + grp * PcCfg<N2>::SLOT, u % ns);
             return;
         }
     }
@@ -387,7 +387,9 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_ker
     const int grp = threadIdx.x / G, t = threadIdx.x % G;
     const int b = (int)blockIdx.x - (N2 ? nblk2 : 0);
     const int u = b * PC::RPB1 + grp, ns = a1.nsub > 1 ? a1.nsub : 1;   // (no FIR when ns > 1)
-    pc_row<TIn, N1, G>(echo, out, a1, u / ns, t, lds + grp * PcCfg<N1>::SLOT, u % ns);
+    // a row of one wave (G == 64) synchronises its exchanges within the wave: the rows of a
+    // workgroup run independently instead of in barrier lockstep
+    pc_row<TIn, N1, G, 0, G == 64>(echo, out, a1, u / ns, t, lds + grp * PcCfg<N1>::SLOT, u % ns);
 }
 
 
