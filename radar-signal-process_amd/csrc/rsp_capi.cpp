@@ -37,6 +37,7 @@ struct rsp_ctx {
     rsp::PcArgs pc{};
     bool pc_v2 = false;                 // per-segment specialised kernels (pc_mf_kernel)
     bool pc_ols_off = false;            // RSP_PC_OLS=0 at create: no overlap-save split (A/B, tests)
+    int pc_ols_min = 8192;              // split segments longer than this (RSP_PC_OLS_MIN at create)
     std::vector<rsp::PcMfArgs> pc_mf;   // one launch per matched-filter segment
     rsp::MtdArgs mtd{};
     int64_t V = 0;                      // Doppler rows (rsp_params.mtd_nfft or P)
@@ -204,9 +205,10 @@ static int pc_overlap_save(rsp_ctx* ctx, const rsp_pc_segment& g, rsp::PcMfArgs&
     a.sub_step = 0;
     const int64_t nfft = a.mf.nfft;
     const int64_t hlen = g.coef_len < nfft ? g.coef_len : nfft;
-    if (nfft <= 8192 || a.do_fir || nfft < (int64_t)a.mf.out_len + hlen - 1) return RSP_OK;
+    if (nfft <= ctx->pc_ols_min || a.do_fir || nfft < (int64_t)a.mf.out_len + hlen - 1) return RSP_OK;
     int best = 0, best_n = 0, best_step = 0;
-    for (int nb : {4096, 8192}) {
+    for (int nb : {8192, 4096, 2048}) {   // (ties: the longer block, fewer re-read samples)
+        if (nb >= nfft) continue;
         const int64_t step = nb - hlen + 1;
         if (step < nb / 2) continue;
         const int64_t n = (a.mf.out_len + step - 1) / step;
@@ -335,6 +337,7 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     ctx->device = device;
     ctx->p = p;
     if (const char* ols = std::getenv("RSP_PC_OLS")) ctx->pc_ols_off = std::atoi(ols) == 0;
+    if (const char* olm = std::getenv("RSP_PC_OLS_MIN")) ctx->pc_ols_min = std::atoi(olm) > 0 ? std::atoi(olm) : 8192;
     for (int s = 0; s < RSP_MAX_SEG; ++s) ctx->p.seg[s].coef_re = ctx->p.seg[s].coef_im = nullptr;
     auto bail = [&](int rc) {
         g_err = ctx->err;
