@@ -293,6 +293,32 @@ def test_full_batch_properties(torch_cuda):
     assert torch.equal(flag2, flag)
 
 
+def test_create_legacy_matches_python_preset(torch_cuda):
+    """rsp_create_legacy (the one-argument MEX path: split and FIR in C, the measured pulses
+    passed in) builds the same context as the Python legacy preset: bit-identical RDMs."""
+    import ctypes as C
+    from rsp import _capi as capi, presets, synth
+    from rsp.engine import Engine
+    P, R = 48, 1031
+    lib = capi.load_library()
+    ctx = C.c_void_p()
+    p2 = presets.load_data("legacy_pulse2").astype(np.complex128)
+    p3 = presets.load_data("legacy_pulse3").astype(np.complex128)
+    arrs = [np.ascontiguousarray(a) for a in (p2.real, p2.imag, p3.real, p3.imag)]
+    dp = [a.ctypes.data_as(C.POINTER(C.c_double)) for a in arrs]
+    assert lib.rsp_create_legacy(C.byref(ctx), 0, P, R, dp[0], dp[1], len(p2), dp[2], dp[3], len(p3)) == 0
+    echo = synth.echo_numpy(presets.legacy(P, R), 2, seed=19).astype(np.complex128)
+    out = np.empty((2, P, R), np.float32)
+    rc = lib.rsp_pc_mtd(ctx, echo.ctypes.data, capi.RSP_C128, capi.RSP_ROWMAJOR, P, R, 2, out.ctypes.data,
+                        capi.RSP_ROWMAJOR)
+    assert rc == 0
+    lib.rsp_destroy(ctx)
+    with Engine(presets.legacy(P, R)) as eng:
+        want = eng.pc_mtd(echo)
+    np.testing.assert_array_equal(out, want)
+    assert lib.rsp_create_legacy(C.byref(ctx), 0, P, 300, dp[0], dp[1], len(p2), dp[2], dp[3], len(p3)) != 0
+
+
 def test_create_v2_matches_python_preset(torch_cuda):
     """rsp_create_v2 (the MEX path: params fields -> context in C) == the Python v2 preset."""
     import ctypes as C
