@@ -608,7 +608,8 @@ struct DopplerOut {
     bool zero_bg;                    // rflag: write the flag plane's zero background here
 };
 
-// The Doppler-stage outputs of a thread's run of N rows (bit i of `mask` = row v0+i is a hit):
+// The Doppler-stage outputs of a thread's run of N rows (bit i of `mask` = row v0+i is a hit);
+// called with every lane of the wave active (its ballots and prefix-sum shuffles read all lanes):
 // flagV / flag bytes where requested (uniform branches, once per run), and the hits appended to
 // the workgroup's list.  Hits are sparse, so the append path is entered only by waves that
 // have one: one ballot over the masks, then per row one ballot and one LDS atomic per wave.
@@ -695,21 +696,39 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
     const bool go = cv.method == 0;
     static_assert(E <= 32, "row mask");
     uint32_t mask = 0;
+    if (kl <= 0 && kr >= E - 1 && b0 <= 0 && b1 >= E && go) {
+        // the common case: every row of the run is tested and has both windows (GO): the same
+        // sums and compare-select as below, without the per-row window and band selects
 #pragma unroll
-    for (int i = 0; i < E; ++i) {
-        float sl = L[i], sr = Rw[i];
+        for (int i = 0; i < E; ++i) {
+            float sl = L[i], sr = Rw[i];
 #pragma unroll
-        for (int q = 1; q < REF; ++q) {
-            sl += L[i + q];
-            sr += Rw[i + q];
+            for (int q = 1; q < REF; ++q) {
+                sl += L[i + q];
+                sr += Rw[i + q];
+            }
+            const float th = (sl > sr ? sl : sr) * cv.Tr;
+            mask |= (m[i] >= th ? 1u : 0u) << i;
         }
-        const bool lok = i >= kl, rok = i <= kr;
-        const float x = lok ? sl : sr, y = rok ? sr : sl;   // one-sided fallback (:30-39)
-        // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
-        const float th = (go ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
-        const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
-        mask |= (hit ? 1u : 0u) << i;
+        if (!col_on) mask = 0u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            float sl = L[i], sr = Rw[i];
+#pragma unroll
+            for (int q = 1; q < REF; ++q) {
+                sl += L[i + q];
+                sr += Rw[i + q];
+            }
+            const bool lok = i >= kl, rok = i <= kr;
+            const float x = lok ? sl : sr, y = rok ? sr : sl;   // one-sided fallback (:30-39)
+            // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
+            const float th = (go ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
+            const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
+            mask |= (hit ? 1u : 0u) << i;
+        }
     }
+    // (outside the divergent branches: the emission's ballots and shuffles need every lane)
     doppler_emit_mask<E>(o, mask);
 }
 
@@ -793,29 +812,30 @@ struct RangeJob57 {
     float x[NX];
     __device__ __forceinline__ void fetch_idx(const MtdArgs& a, int rg) {
         // both loads issue at once: a region holds W*P >= blockDim entries, so the index load
-        // is in bounds (and ignored) past the count -- no count -> index round trip ahead of
-        // the tile's own loads
+        // is in bounds (and ignored) past the count -- no count -> index round trip
         n = a.prev_count[rg];
         idx = a.prev_hits[(size_t)rg * a.prev_region + threadIdx.x];
     }
     __device__ __forceinline__ void fetch_cells(const MtdArgs& a) {
+        // Every wave of every MTD workgroup issues these 27 loads, unconditionally: a lane
+        // without a cell (no hit, no job) loads through the buffer range check (voffset kOob:
+        // 0, no memory access).  A branch around them would leave the waits of the tile's FFT
+        // (vmcnt counts in issue order) merged from two paths, so a wave with hits would wait
+        // for its gathers before its first butterfly (c3: 3.8 us per 16-CPI launch).
         const CfarRArgs& c = a.prev_cr;
         const bool mine = threadIdx.x < n;
-        if (!__ballot(mine)) return;   // (wave-uniform) no hit in this wave
-        const uint32_t row = idx / (uint32_t)c.R;
-        const int r = (int)(idx - row * (uint32_t)c.R);
-        const int v = (int)(row % (uint32_t)c.V);
+        const uint32_t R = c.R > 0 ? (uint32_t)c.R : 1u, V = c.V > 0 ? (uint32_t)c.V : 1u;   // (no job: unset)
+        const uint32_t row = idx / R;
+        const int r = (int)(idx - row * R);
+        const int v = (int)(row % V);
         const bool zrow = v >= c.cz_lo && v < c.cz_hi;
-        const float* xr = a.prev_rdm + (size_t)row * c.R;
-        // branch-free: every lane of the wave loads (a clamped address), then selects; with no
-        // per-cell branch the loads stay here, ahead of the tile's FFT, and are waited on in finish()
+        const auto rr = buf_rsrc(a.prev_rdm, kOob);   // job => the chunk's RDM is < kOob bytes
+        const uint32_t rowoff = row * R;
 #pragma unroll
         for (int k = 0; k < NX; ++k) {
             const int q = r - H + k;
             const bool ok = mine && !zrow && q >= 0 && q < c.R;
-            const float* p = ok ? xr + q : a.prev_rdm;
-            const float val = *p;
-            x[k] = ok ? val : 0.f;
+            x[k] = buf_ld_f(rr, ok ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
         }
     }
     __device__ __forceinline__ void finish(const MtdArgs& a) {
@@ -983,6 +1003,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         mag[v] = (v >= a.cv.cz_lo && v < a.cv.cz_hi) ? 0.f : mg[m];   // main_cfar.m:90-91
     }
     __syncthreads();
+
     const int v0 = g * E;   // this thread's run of Doppler rows
     const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
     DopplerOut o;
@@ -1049,17 +1070,17 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) voi
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
     const int nwg = (int)(gridDim.x * gridDim.y);
-    const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions;
-    if (job) {
-        RangeJob57 rj;
-        rj.fetch_idx(a, (int)wg);
-        mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits, [&] { rj.fetch_cells(a); });
-        rj.finish(a);
-        if (rj.n > blockDim.x || a.prev_nregions > nwg) prev_chunk_hits(a, (int)wg, nwg, (int)blockDim.x);
-    } else {
-        mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits);
-        if (a.prev_nregions > 0) prev_chunk_hits(a, (int)wg, nwg, 0);
-    }
+    // one instance of the tile (the kernel's code stays ~half the size: it shares the
+    // instruction cache with the PC kernel of the other pipeline); the range job is runtime-
+    // guarded -- with n == 0 its hook and finish() return at once
+    const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions &&
+                     (uint64_t)a.prev_nregions * (uint64_t)a.prev_region < (uint64_t)(kOob / 4u);
+    RangeJob57 rj;
+    if (job) rj.fetch_idx(a, (int)wg);
+    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits, [&] { rj.fetch_cells(a); });
+    rj.finish(a);
+    if (job ? (rj.n > blockDim.x || a.prev_nregions > nwg) : a.prev_nregions > 0)
+        prev_chunk_hits(a, (int)wg, nwg, job ? (int)blockDim.x : 0);
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
