@@ -599,8 +599,10 @@ def main():
                 "note": "one step = one launch sequence over the batch; achieved = units/s (device events "
                         "around the timed steps) x alg bytes per unit"}
         if pmc and pmc.get("bytes_per_unit"):
-            roof["traffic"] = int(pmc["bytes_per_unit"])
-            roof["traffic_per"] = "unit (CPI or window), all kernels of a profiled run"
+            # per launch like `achieved` (one launch sequence = one step of `units` CPIs/windows)
+            roof["traffic"] = int(pmc["bytes_per_unit"] * units)
+            roof["traffic_per"] = "step (units_per_launch units), all kernels, from a profiled run's bytes per unit"
+            roof["traffic_per_unit"] = int(pmc["bytes_per_unit"])
             roof["traffic_ratio"] = round(pmc["bytes_per_unit"] / cpi_bytes, 3)
             roof["traffic_source"] = "profiles/pmc_%s.json" % tag
         if kernels:
