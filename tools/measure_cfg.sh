@@ -20,6 +20,13 @@ tail -1 "$OUT/bench.log" | python -c "import json,sys; d=json.loads(sys.stdin.re
     || { echo "rocprof rc=$?"; tail -3 "$OUT/prof.log"; exit 1; }
 python tools/trace_summary.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/trace.json" > /dev/null
 python -c "import json; d=json.load(open('$OUT/trace.json')); print('trace span ms/step', d['span_ms_per_step'], {k: v['avg_us'] for k, v in d['kernels'].items()})"
+# the same on ONE pipeline (--streams 1): kernels do not overlap, so rocprof's per-kernel averages
+# are comparable with bench.py's single-pipeline per-kernel entries
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof1" -o run -- \
+    python3 "$ROOT/bench.py" --config $CFG --steps 5 --warmup 1 --cpu-seconds 0 --no-profile --streams 1 $EXTRA > "$OUT/prof1.log" 2>&1) \
+    || { echo "rocprof (1 pipeline) rc=$?"; tail -3 "$OUT/prof1.log"; exit 1; }
+python tools/trace_summary.py "$OUT/prof1/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/trace_1lane.json" > /dev/null
+python -c "import json; d=json.load(open('$OUT/trace_1lane.json')); print('1-pipeline trace', d['span_ms_per_step'], {k: v['avg_us'] for k, v in d['kernels'].items()})"
 [ "${PMC:-1}" = "1" ] || exit 0
 PSTEPS=${PMC_STEPS:-2}
 PGROUPS=("FETCH_SIZE" "WRITE_SIZE")

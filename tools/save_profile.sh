@@ -9,5 +9,8 @@ dst="$ROOT/profiles/$1/$2"; src="$ROOT/gpurun_out/$2"
 mkdir -p "$dst"
 cp "$src/bench.log" "$src/trace.json" "$src/pmc.json" "$src/pmc.txt" "$dst/"
 cp "$src/prof/run_kernel_stats.csv" "$dst/kernel_stats.csv"
+if [ -f "$src/prof1/run_kernel_stats.csv" ]; then
+  cp "$src/prof1/run_kernel_stats.csv" "$dst/kernel_stats_1pipeline.csv"; cp "$src/trace_1lane.json" "$dst/"
+fi
 cp "$src/pmc.json" "$ROOT/profiles/pmc_$3.json"
 echo "saved $2 -> profiles/$1/$2, profiles/pmc_$3.json"
