@@ -312,3 +312,72 @@ def test_fp16_tolerance_sweep(torch_cuda):
             base = min(q["storage_rel_err"] for q in rows if q["snr_db"] == r["snr_db"] and q["usable"])
             assert r["storage_rel_err"] > 2.0 * base, r
     assert all(r["nonfinite"] > 0 for r in rows if r["scale"] == 2.0 ** 12)
+
+
+# ---------------------------------------------------------------- full BASELINE sizes
+def test_c5_full_batch_properties(torch_cuda):
+    """c5 at the bench's full size (64 fp16 CPIs of 512 x 16384: 64 one-CPI chunks through both
+    pipelines, overlap-save PC): spot CPIs against the oracle fed the same fp16 samples, and the
+    exact size-independent property RDM(2x) = 2 RDM(x), flags unchanged (scaling fp16 I/Q by 2
+    is exact, and so is every fp32 operation after it)."""
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    P, R, B = 512, 16384, 64
+    spec = presets.v2(P, R)
+    cf = presets.default_cfar(spec)
+    eng = Engine(spec, device=0)
+    echo = synth.echo_torch(spec, B, seed=2025, half=True)
+    rdm = torch.empty((B, P, R), dtype=torch.float32, device="cuda")
+    flag = torch.empty((B, P, R), dtype=torch.uint8, device="cuda")
+    eng.run_dev(echo, rdm=rdm, flag=flag, cfar=cf)
+    torch.cuda.synchronize()
+    for i in (0, 37, 63):
+        h = echo[i].cpu().numpy().astype(np.float64)
+        want = oracle_rdm("v2", (h[..., 0] + 1j * h[..., 1])[None])
+        assert rel_err(rdm[i].cpu().numpy()[None], want) < RDM_TOL, i
+        wflag, _, amb = oracle_flags_c(want, cf)
+        hard, soft = flag_mismatch(flag[i].cpu().numpy()[None], wflag, amb)
+        assert hard == 0 and soft <= max(2, wflag.size // 100000), (i, hard, soft)
+    rdm2 = torch.empty_like(rdm)
+    flag2 = torch.empty_like(flag)
+    echo.mul_(2.0)
+    eng.run_dev(echo, rdm=rdm2, flag=flag2, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(rdm2, rdm * 2.0)
+    assert torch.equal(flag2, flag)
+    eng.close()
+
+
+def test_c4_full_stream_properties(torch_cuda):
+    """c4 at the bench's full size (32 frame pairs x 4 windows of 256 x 8192): spot windows
+    against the oracle on the sliced echo, and RDM(2x) = 2 RDM(x) with flags unchanged."""
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    P, R, F, W = 256, 8192, 32, 4
+    spec = presets.v2(P, R)
+    cf = presets.default_cfar(spec)
+    eng = Engine(spec, device=0)
+    frames = synth.echo_torch(spec, F + 1, seed=2026).reshape(1, F + 1, P, R)
+    shp = (1, F, W, P, R)
+    rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.window_dev(frames, W, rdm=rdm, flag=flag, cfar=cf)
+    torch.cuda.synchronize()
+    for n, i in ((0, 0), (17, 3), (31, 2)):
+        s = _mround(i * P / W)
+        pair = torch.cat([frames[0, n], frames[0, n + 1]], dim=0)[s:s + P].cpu().numpy()
+        want = oracle_rdm("v2", pair[None])
+        assert rel_err(rdm[0, n, i].cpu().numpy()[None], want) < RDM_TOL, (n, i)
+        wflag, _, amb = oracle_flags_c(want, cf)
+        hard, soft = flag_mismatch(flag[0, n, i].cpu().numpy()[None], wflag, amb)
+        assert hard == 0 and soft <= max(2, wflag.size // 100000), (n, i, hard, soft)
+    rdm2 = torch.empty_like(rdm)
+    flag2 = torch.empty_like(flag)
+    frames.mul_(2.0)
+    eng.window_dev(frames, W, rdm=rdm2, flag=flag2, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(rdm2, rdm * 2.0)
+    assert torch.equal(flag2, flag)
+    eng.close()
