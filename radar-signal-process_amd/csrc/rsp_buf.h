@@ -37,13 +37,10 @@ __device__ __forceinline__ void buf_st_u8(uint8_t v, __amdgpu_buffer_rsrc_t r, u
     __builtin_amdgcn_raw_buffer_store_b8(v, r, voff, soff, 0);
 }
 
-// Cache policy of the streamed-once planes (echo input, RDM output).  -DRSP_NT=2 marks them
-// non-temporal (aux bit 1, `nt`) so they would not evict the PC scratch; measured slower (the
-// range stage re-reads RDM neighbourhoods, and PC gains nothing), so the default is 0.
-#ifndef RSP_NT
-#define RSP_NT 0
-#endif
-constexpr int kStreamAux = RSP_NT;
+// Cache policy of the streamed-once planes (echo input, RDM output): the default.  Marking
+// them non-temporal (aux bit 1, `nt`) so they would not evict the PC scratch was measured
+// slower (the range stage re-reads RDM neighbourhoods, and PC gains nothing).
+constexpr int kStreamAux = 0;
 
 // one complex element of an input plane (complex fp32, or fp16 I/Q widened on load)
 __device__ __forceinline__ float2 buf_ld_c(const float2*, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {

@@ -369,16 +369,11 @@ __device__ __forceinline__ void fft_reg(float2 (&u)[E], float2* buf, int t, cons
 // together with the row's input loads so their latency overlaps) and every pass reads
 // them from registers instead of waiting on table loads after each LDS exchange.
 //
-// RSP_TW_LEAN (default): a thread keeps only the base twiddles W^e (and W^4e for radix 8/16)
-// of each butterfly and forms the other powers with complex products when it applies them
-// (radix 16: W^2e = (W^e)^2, W^3e, W^8e = (W^4e)^2, W^12e; ~2-4 ulp) -- 8 VGPRs instead of
-// 24 for a 4096-point row of E = 16, so more rows stay resident per SIMD.
-#ifndef RSP_TW_LEAN
-#define RSP_TW_LEAN 1
-#endif
-__host__ __device__ constexpr int tw_loads(int R) {
-    return RSP_TW_LEAN ? (R >= 8 ? 2 : 1) : (R == 16 ? 6 : R == 8 ? 4 : R - 1);
-}
+// Lean twiddles: a thread keeps only the base twiddles W^e (and W^4e for radix 8/16) of each
+// butterfly and forms the other powers with complex products when it applies them (radix 16:
+// W^2e = (W^e)^2, W^3e, W^8e = (W^4e)^2, W^12e; ~2-4 ulp) -- 8 VGPRs instead of 24 for a
+// 4096-point row of E = 16, so more rows stay resident per SIMD.
+__host__ __device__ constexpr int tw_loads(int R) { return R >= 8 ? 2 : 1; }
 
 template <int N, int E>
 __host__ __device__ constexpr int tw_regs(int Ns = 1) {
@@ -393,24 +388,14 @@ __host__ __device__ constexpr int tw_regs(int Ns = 1) {
 
 template <int R>
 __device__ __forceinline__ void tw_fetch(float2* w, int e, const float2* __restrict__ tw) {
-    if constexpr (RSP_TW_LEAN) {
-        w[0] = tw[e];
-        if constexpr (R >= 8) w[1] = tw[4 * e];
-    } else if constexpr (R == 16) {
-        w[0] = tw[e]; w[1] = tw[2 * e]; w[2] = tw[3 * e];
-        w[3] = tw[4 * e]; w[4] = tw[8 * e]; w[5] = tw[12 * e];
-    } else if constexpr (R == 8) {
-        w[0] = tw[e]; w[1] = tw[2 * e]; w[2] = tw[3 * e]; w[3] = tw[4 * e];
-    } else {
-#pragma unroll
-        for (int r = 1; r < R; ++r) w[r - 1] = tw[r * e];
-    }
+    w[0] = tw[e];
+    if constexpr (R >= 8) w[1] = tw[4 * e];
 }
 
 // v[r] *= W^(r*e) from the tw_fetch<R> entries (same products as twiddle<R, N>)
 template <int R>
 __device__ __forceinline__ void tw_apply(float2* v, const float2* w) {
-    if constexpr (RSP_TW_LEAN && R == 16) {
+    if constexpr (R == 16) {
         // opaque copies: the derived powers are formed at every use instead of being hoisted
         // out of a row loop into registers (which would undo the saving)
         float2 w1 = w[0], w4 = w[1];
@@ -431,7 +416,7 @@ __device__ __forceinline__ void tw_apply(float2* v, const float2* w) {
         v[13] = cmul(v[13], cmul(w12, w1));
         v[14] = cmul(v[14], cmul(w12, w2));
         v[15] = cmul(v[15], cmul(w12, w3));
-    } else if constexpr (RSP_TW_LEAN && R == 8) {
+    } else if constexpr (R == 8) {
         float2 w1 = w[0], w4 = w[1];
         asm volatile("" : "+v"(w1), "+v"(w4));
         const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
@@ -442,7 +427,7 @@ __device__ __forceinline__ void tw_apply(float2* v, const float2* w) {
         v[5] = cmul(v[5], cmul(w4, w1));
         v[6] = cmul(v[6], cmul(w4, w2));
         v[7] = cmul(v[7], cmul(w4, w3));
-    } else if constexpr (RSP_TW_LEAN) {
+    } else {
         float2 w0 = w[0];
         asm volatile("" : "+v"(w0));
         float2 wr = w0;
@@ -451,35 +436,6 @@ __device__ __forceinline__ void tw_apply(float2* v, const float2* w) {
             v[r] = cmul(v[r], wr);
             if (r + 1 < R) wr = cmul(wr, w0);
         }
-    } else if constexpr (R == 16) {
-        const float2 w1 = w[0], w2 = w[1], w3 = w[2], w4 = w[3], w8 = w[4], w12 = w[5];
-        v[1] = cmul(v[1], w1);
-        v[2] = cmul(v[2], w2);
-        v[3] = cmul(v[3], w3);
-        v[4] = cmul(v[4], w4);
-        v[5] = cmul(v[5], cmul(w4, w1));
-        v[6] = cmul(v[6], cmul(w4, w2));
-        v[7] = cmul(v[7], cmul(w4, w3));
-        v[8] = cmul(v[8], w8);
-        v[9] = cmul(v[9], cmul(w8, w1));
-        v[10] = cmul(v[10], cmul(w8, w2));
-        v[11] = cmul(v[11], cmul(w8, w3));
-        v[12] = cmul(v[12], w12);
-        v[13] = cmul(v[13], cmul(w12, w1));
-        v[14] = cmul(v[14], cmul(w12, w2));
-        v[15] = cmul(v[15], cmul(w12, w3));
-    } else if constexpr (R == 8) {
-        const float2 w1 = w[0], w2 = w[1], w3 = w[2], w4 = w[3];
-        v[1] = cmul(v[1], w1);
-        v[2] = cmul(v[2], w2);
-        v[3] = cmul(v[3], w3);
-        v[4] = cmul(v[4], w4);
-        v[5] = cmul(v[5], cmul(w4, w1));
-        v[6] = cmul(v[6], cmul(w4, w2));
-        v[7] = cmul(v[7], cmul(w4, w3));
-    } else {
-#pragma unroll
-        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], w[r - 1]);
     }
 }
 
