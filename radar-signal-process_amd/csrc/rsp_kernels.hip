@@ -24,6 +24,11 @@
 #include "rsp_buf.h"
 #include "rsp_internal.h"
 
+
+#ifndef RSP_MTD_TS
+#define RSP_MTD_TS 256
+#endif
+
 namespace rsp {
 
 __device__ __forceinline__ float2 ld_c(const float2* p) { return *p; }
@@ -263,11 +268,13 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
                                        const PcMfArgs& a, int row, int t, float2* buf, int sub = 0) {
     constexpr int E = N / G;
     constexpr bool kUniform = G % 64 == 0;
-    // Short rows (G <= 64, the segment that also carries the FIR): every global load of the
-    // row -- MF input and the whole spectrum slice -- is issued before the FIR, so one memory
-    // round trip overlaps the FIR instead of three in sequence.  Long rows keep the spectrum
-    // loads after the forward FFT (32 fewer live VGPRs across it).
-    constexpr bool kEarly = G <= 64;
+    // Every global load of the row -- MF input and the whole spectrum slice -- is issued up
+    // front, so one memory round trip overlaps the FIR (short rows) and the spectrum arrives
+    // during the forward FFT instead of after it (N <= 4096: the 32 extra live VGPRs fit the
+    // paired kernel's allocation, which its short-row path already sets; PC 41 -> 39.8 us per
+    // 16 CPIs at c3, 39.7 -> 37.8 us per CPI at c5).  8192/16384-point rows keep the spectrum
+    // loads after the forward FFT.
+    constexpr bool kEarly = G <= 64 || N <= 4096;
     if constexpr (kUniform) {   // (a VGPR-held offset in a buffer resource means a waterfall loop per access)
         row = __builtin_amdgcn_readfirstlane(row);
         sub = __builtin_amdgcn_readfirstlane(sub);
@@ -569,7 +576,8 @@ struct MtdCfg {
     static constexpr int E = (P % 3 == 0) ? 24 : 16;
     static constexpr int G = P / E;                    // threads per range bin
     // threads per workgroup (512 for P = 256 measured neutral at c4: 529 vs 523 us per launch)
-    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024) : kBlock;
+    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024)
+                           : (BEAMS == 1 && P == 128) ? RSP_MTD_TS : kBlock;
     // minimum waves per SIMD (__launch_bounds__' second argument): two 512-thread workgroups
     // per CU need <= 128 VGPRs
     static constexpr int WPE = T == 512 ? 4 : 1;
@@ -1069,6 +1077,13 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) voi
     T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
+    {   // 4 consecutive tiles on one XCD (workgroup x goes to XCD x % 8): their partial RDM /
+        // flag lines (W = 16: 64-B RDM and 16-B flag row segments at c5) meet in one L2 and leave
+        // it merged (c5 +1.5-2 %, c3 neutral)
+        constexpr int K = 4;
+        const int x = (int)blockIdx.x;
+        if (gridDim.x % (8 * K) == 0) T.bx = (x / (8 * K)) * (8 * K) + (x % 8) * K + (x / 8) % K;
+    }
     const int nwg = (int)(gridDim.x * gridDim.y);
     // one instance of the tile (the kernel's code stays ~half the size: it shares the
     // instruction cache with the PC kernel of the other pipeline); the range job is runtime-
@@ -1900,7 +1915,9 @@ template <typename TIn, int N1, int N2, int P, int REF>
 __global__ __launch_bounds__(kBlock, 2) void chain_kernel(ChainArgs a) {
     using CC = ChainCfg<N1, N2, P>;
     static_assert(CC::PC::T == kBlock && PcCfg<N2>::G == kBlock, "one long-segment row per workgroup");
+#if RSP_MTD_TS == 256
     static_assert(CC::MC::W * CC::MC::G == kBlock, "MTD tile shape");
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* sw = reinterpret_cast<uint32_t*>(smem + ((CC::main + 15) & ~(size_t)15));   // [0] item, [1] hits
     const int tid = threadIdx.x;
