@@ -25,10 +25,6 @@
 #include "rsp_internal.h"
 
 
-#ifndef RSP_MTD_TS
-#define RSP_MTD_TS 256
-#endif
-
 namespace rsp {
 
 __device__ __forceinline__ float2 ld_c(const float2* p) { return *p; }
@@ -576,8 +572,7 @@ struct MtdCfg {
     static constexpr int E = (P % 3 == 0) ? 24 : 16;
     static constexpr int G = P / E;                    // threads per range bin
     // threads per workgroup (512 for P = 256 measured neutral at c4: 529 vs 523 us per launch)
-    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024)
-                           : (BEAMS == 1 && P == 128) ? RSP_MTD_TS : kBlock;
+    static constexpr int T = (BEAMS == 1 && P >= 512 && P % 3 != 0) ? (G * 16 < 1024 ? G * 16 : 1024) : kBlock;
     // minimum waves per SIMD (__launch_bounds__' second argument): two 512-thread workgroups
     // per CU need <= 128 VGPRs
     static constexpr int WPE = T == 512 ? 4 : 1;
@@ -1077,9 +1072,10 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) voi
     T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = blockIdx.x;
-    {   // 4 consecutive tiles on one XCD (workgroup x goes to XCD x % 8): their partial RDM /
-        // flag lines (W = 16: 64-B RDM and 16-B flag row segments at c5) meet in one L2 and leave
-        // it merged (c5 +1.5-2 %, c3 neutral)
+    if constexpr (C::W < 32) {   // 4 consecutive tiles on one XCD (workgroup x goes to XCD x % 8):
+        // their partial RDM / flag lines (W = 16: 64-B RDM and 16-B flag row segments at c5)
+        // meet in one L2 and leave it merged (c5 +1.5-2 %; at W = 32 the RDM segments are whole
+        // 128-B lines and the grouping cost c3's MTD 3 %)
         constexpr int K = 4;
         const int x = (int)blockIdx.x;
         if (gridDim.x % (8 * K) == 0) T.bx = (x / (8 * K)) * (8 * K) + (x % 8) * K + (x / 8) % K;
@@ -1915,9 +1911,7 @@ template <typename TIn, int N1, int N2, int P, int REF>
 __global__ __launch_bounds__(kBlock, 2) void chain_kernel(ChainArgs a) {
     using CC = ChainCfg<N1, N2, P>;
     static_assert(CC::PC::T == kBlock && PcCfg<N2>::G == kBlock, "one long-segment row per workgroup");
-#if RSP_MTD_TS == 256
     static_assert(CC::MC::W * CC::MC::G == kBlock, "MTD tile shape");
-#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* sw = reinterpret_cast<uint32_t*>(smem + ((CC::main + 15) & ~(size_t)15));   // [0] item, [1] hits
     const int tid = threadIdx.x;
