@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import rsp_ref as ref
-from _util import NEAR_TOL, RDM_TOL, flag_mismatch, oracle_flags, oracle_rdm, rel_err
+from _util import NEAR_TOL, RDM_TOL, flag_mismatch, oracle_flags, oracle_flags_c, oracle_rdm, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -340,3 +340,28 @@ def test_create_v2_matches_python_preset(torch_cuda):
         want = eng.pc_mtd(echo)
     assert rel_err(out, want) < 1e-6
     assert rel_err(out, oracle_rdm("v2", echo)) < RDM_TOL
+
+
+@pytest.mark.parametrize("P,R", [(256, 3000), (512, 2048)])
+def test_chain_cfar_tile_mappings(torch_cuda, P, R):
+    """MTD tiles narrower than a cache line (W = 16) are grouped 4 per XCD when the tile count
+    is a multiple of 32 (512 x 2048: 128 tiles) and mapped in order otherwise (256 x 3000: 188
+    tiles, R % 16 != 0 so the flag background is written per cell): both against the oracle."""
+    torch = torch_cuda
+    from rsp import presets
+    eng = _engine("v2", P, R)
+    cf = presets.default_cfar(eng.spec)
+    echo = _echo(eng, 2)
+    d_in = torch.from_numpy(echo).cuda()
+    shp = (2, P, R)
+    d_rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm, flag=d_flag, cfar=cf)
+    torch.cuda.synchronize()
+    rdm = oracle_rdm("v2", echo)
+    assert rel_err(d_rdm.cpu().numpy(), rdm) < RDM_TOL
+    flag, _, amb = oracle_flags_c(rdm, cf)
+    hard, soft = flag_mismatch(d_flag.cpu().numpy(), flag, amb)
+    assert hard == 0, (hard, soft)
+    assert soft <= max(2, flag.size // 100000), soft
+    assert flag.sum() > 0
