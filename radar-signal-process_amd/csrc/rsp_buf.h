@@ -42,12 +42,17 @@ __device__ __forceinline__ void buf_st_u8(uint8_t v, __amdgpu_buffer_rsrc_t r, u
 // slower (the range stage re-reads RDM neighbourhoods, and PC gains nothing).
 constexpr int kStreamAux = 0;
 
-// one complex element of an input plane (complex fp32, or fp16 I/Q widened on load)
+// one complex element of an input plane (complex fp32, or fp16 I/Q widened on load).  The fp16
+// echo (config c5: 512 x 16384, a 67 MB PC scratch per CPI and pipeline, near the 256 MB
+// Infinity Cache with two pipelines) is loaded non-temporal (aux bit 1, `nt`): read once, it
+// then evicts less of the scratch (c5 +2 %).  The same hint on the fp32 echo was neutral at c3
+// and cost c4 3 %, and on the MTD's scratch loads cost c3 2 % and c5 2 %.
+constexpr int kEchoF16Aux = 2;
 __device__ __forceinline__ float2 buf_ld_c(const float2*, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kStreamAux));
 }
 __device__ __forceinline__ float2 buf_ld_c(const __half2*, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kStreamAux)));
+    return __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kEchoF16Aux)));
 }
 // streamed-once store (RDM)
 __device__ __forceinline__ void buf_st_f_stream(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
