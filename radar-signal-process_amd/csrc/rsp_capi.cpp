@@ -975,7 +975,8 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     int64_t cu = chunk_of(ctx, units * ocpi);              // CPIs per chunk
     if (win > 0) {
         cu = cu / ocpi;
-        if (cu < 8) cu = 8;                                // look-ahead PC overhead <= 1/8
+        if (ctx->chunk > 0) cu = cu > 0 ? cu : 1;          // explicit chunk (rsp_set_chunk): as asked
+        else if (cu < 8) cu = 8;                           // look-ahead PC overhead <= 1/8
     }
     if (cu > units) cu = units;
     const int64_t nchunks = (units + cu - 1) / cu;
