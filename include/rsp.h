@@ -176,10 +176,10 @@ const char* rsp_last_error(const rsp_ctx* ctx);
 /* CPIs processed per internal chunk (PC scratch = chunk * P * R_out * 8 bytes, sized to
  * stay in the 256 MiB Infinity Cache).  0 restores the default.  Window mode counts output
  * windows: chunk / windows frame pairs per chunk (each chunk also pulse-compresses one
- * look-ahead frame); the default there is at least 8 pairs. */
+ * look-ahead frame); the default there is at least 16 pairs. */
 int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 
-/* Number of chunk pipelines (1..4, default 2): chunk k runs on the caller's stream or on
+/* Number of chunk pipelines (1..4; default 2, window mode 1): chunk k runs on the caller's stream or on
  * one of n-1 context-owned streams that fork from and join back into it, so consecutive
  * chunks overlap.  Each pipeline owns one PC scratch slot. */
 int rsp_set_streams(rsp_ctx* ctx, int32_t n);

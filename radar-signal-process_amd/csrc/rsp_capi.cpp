@@ -44,7 +44,7 @@ struct rsp_ctx {
     int beams = 1;                      // 2: DMX left/right pair
     size_t pc_lds = 0;
     int64_t chunk = 0;  // 0 = default
-    int nstreams = 2;   // chunk pipelines (the caller's stream + nstreams-1 internal ones)
+    int nstreams = 0;   // chunk pipelines (the caller's stream + nstreams-1 internal ones); 0 = default
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
     // The context's scratch (PC corner turn, hit lists, internal RDM, flagV staging) is reused by
@@ -973,14 +973,18 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     m.nwin = win;
     for (int i = 0; i < win; ++i) m.win_start[i] = (int)mround((double)i * P / win);
     int64_t cu = chunk_of(ctx, units * ocpi);              // CPIs per chunk
+    // Default pipelines: 2 (PC of one chunk overlaps MTD / CFAR of the other); window mode 1 with
+    // chunks of >= 16 frame pairs (look-ahead PC overhead <= 1/16): c4 98-99k windows/s against
+    // 94k with 2 pipelines of 8 pairs, whose 2 x 144 MiB of scratch overflows the Infinity Cache
+    const int nsd = ctx->nstreams > 0 ? ctx->nstreams : (win > 0 ? 1 : 2);
     if (win > 0) {
         cu = cu / ocpi;
         if (ctx->chunk > 0) cu = cu > 0 ? cu : 1;          // explicit chunk (rsp_set_chunk): as asked
-        else if (cu < 8) cu = 8;                           // look-ahead PC overhead <= 1/8
+        else if (cu < 16) cu = 16;
     }
     if (cu > units) cu = units;
     const int64_t nchunks = (units + cu - 1) / cu;
-    const int ns = (int)(ctx->nstreams < nchunks ? ctx->nstreams : nchunks);
+    const int ns = (int)(nsd < nchunks ? nsd : nchunks);
     const size_t plane = (size_t)V * Ro;                  // output cells per CPI
     const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
     const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * NB * P;
