@@ -63,14 +63,19 @@ def parse():
     ap.add_argument("--prefilter", action="store_true",
                     help="fused iSTC (a synthetic stc curve) + MTI lag 30 in the chain (rsp_set_prefilter)")
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
-    ap.add_argument("--fused", type=int, default=0, choices=[0, 1],
-                    help="1: one-launch fused chain where the shape has one; 0: chunked pipeline (library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--profile-every", type=int, default=7,
                     help="(unused; kept for old command lines)")
     ap.add_argument("--lane-steps", type=int, default=2,
                     help="steps of the single-lane per-kernel pass after the timed region (0 = skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo collectives, a stub step; checks the rank launcher, shards and halo")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on device 0, gloo collectives (value not a result)")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher test hook
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="--gpus N launcher: seconds before the ranks are stopped")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.P = args.P or cfg["P"]
@@ -244,7 +249,7 @@ def bench_ingest(args, world, rank, local, dev, dist):
     if world > 1:
         elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         # the fp64 oracle restatement of FrameDataRead_xzr.m on one host thread
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import ingest_ref
@@ -336,7 +341,7 @@ def bench_prefilter(args, world, rank, local, dev, dist):
     if world > 1:
         elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import prefilter_ref
         hx = x[:4].cpu().numpy().astype(np.complex128)
@@ -437,7 +442,7 @@ def bench_measure(args, world, rank, local, dev, dist):
     if world > 1:
         elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import measure_ref
         hs, hd, hf = s[0].double().cpu().numpy(), d[0].double().cpu().numpy(), f[0].cpu().numpy()
@@ -482,20 +487,159 @@ def bench_measure(args, world, rank, local, dev, dist):
         dist.destroy_process_group()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): start
+    N ranks of this script as child processes, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE =
+    N, rendezvous on 127.0.0.1), before this process touches any GPU.  Rank 0's JSON line is
+    checked (n_gpus == N) and printed as this process's one line; the exit status is non-zero
+    when any rank fails, the ranks outlive --launch-timeout, or the line is missing or wrong.
+    The stream each rank processes is its contiguous shard of the frame loop of
+    MTD/main_produce_dataset_win_xzr_v2.m:70-166 (rank_plan); no data crosses ranks."""
+    import subprocess
+    import threading
+    n = args.gpus
+    port = _free_port()
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+
+    def drain():
+        for line in procs[0].stdout:
+            lines.append(line)
+    reader = threading.Thread(target=drain, daemon=True)
+    reader.start()
+    t0, failed = time.time(), None
+    while any(p.poll() is None for p in procs):
+        bad = [r for r, p in enumerate(procs) if p.poll() not in (None, 0)]
+        if bad:
+            failed = "rank %d exited with status %d" % (bad[0], procs[bad[0]].returncode)
+            break
+        if time.time() - t0 > args.launch_timeout:
+            failed = "ranks still running after %.0f s" % args.launch_timeout
+            break
+        time.sleep(0.2)
+    if failed:
+        for p in procs:              # the exact child processes this launcher started
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    reader.join(timeout=30)
+    rcs = [p.wait() for p in procs]
+    if failed is None and any(rcs):
+        r = next(i for i, c in enumerate(rcs) if c)
+        failed = "rank %d exited with status %d" % (r, rcs[r])
+    out = None
+    for line in reversed(lines):
+        if line.lstrip().startswith("{"):
+            out = json.loads(line)
+            break
+    if failed is None and out is None:
+        failed = "rank 0 printed no JSON line"
+    if failed is None and out.get("n_gpus") != n:
+        failed = "rank 0 reported n_gpus=%s, expected %d" % (out.get("n_gpus"), n)
+    if failed:
+        print("bench.py --gpus %d: %s" % (n, failed), file=sys.stderr, flush=True)
+        return 1
+    out["launcher"] = "bench.py --gpus %d: %d child processes, one per GPU (RANK = LOCAL_RANK = r)" % (n, n)
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def rank_plan(args, rank):
+    """The contiguous shard of the unit stream one rank processes (weak scaling):
+    CPIs [lo, hi), or in window mode frame pairs [lo, hi) plus the look-ahead (halo) frame hi,
+    which the next rank owns; the synthetic echo seed follows the first frame or CPI, so the
+    data of a shard does not depend on the number of ranks."""
+    from rsp import shard
+    cfg_id = int(args.config[1:]) if args.config[1:].isdigit() else 0
+    lo, hi = shard.weak_shard(args.batch, rank)
+    if args.win:
+        flo, fhi = shard.window_frames(lo, hi)
+        return {"rank": rank, "frame_pairs": [lo, hi], "frames": [flo, fhi], "halo_frame": fhi - 1,
+                "windows": [lo * args.win, hi * args.win], "seed": 1000 + cfg_id + flo}
+    return {"rank": rank, "cpis": [lo, hi], "seed": 1000 + cfg_id + lo}
+
+
+def dry_run(args, world, rank, dist):
+    """--dry-run: the multi-rank path without a GPU -- gloo rendezvous, each rank's shard plan,
+    a stub step (sleep), barrier + max-over-ranks timing, the per-rank step times and the JSON
+    line, so the launcher, sharding and halo are testable on CPU (tests/test_bench_launch.py)."""
+    from rsp import shard
+    plan = rank_plan(args, rank)
+    if rank == args.dry_run_fail_rank:
+        raise SystemExit("dry run: rank %d fails on request" % rank)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (1 + rank))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    per_rank = shard.gather_over_ranks(elapsed, dist if world > 1 else None)
+    plans = [None] * world
+    if world > 1:
+        dist.all_gather_object(plans, plan)
+    else:
+        plans = [plan]
+    if rank == 0:
+        units = args.batch * (args.win or 1)
+        print(json.dumps({
+            "metric": "dry run (no GPU): launcher, shard plan and halo only", "value": round(world * units * args.steps / max(per_rank), 1),
+            "unit": "window/s" if args.win else "CPI/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(max(per_rank) / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dry_run": True, "config": {"workload": args.config, "batch_per_gpu": args.batch},
+            "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank], "shards": plans}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     args.warmup = max(args.warmup, 1)
-    import torch
-    import torch.distributed as dist
-    from rsp import presets, shard, synth
-    from rsp.engine import Engine
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr, flush=True)
+        sys.exit(2)
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.dry_run or args.share_device:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    if args.dry_run:
+        return dry_run(args, world, rank, dist)
+    from rsp import presets, shard, synth
+    from rsp.engine import Engine
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.config == "ingest":
@@ -508,7 +652,6 @@ def main():
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
-    eng.set_fused(args.fused)
     if args.prefilter:
         import numpy as np
         from rsp.prefilter import istc_gain
@@ -518,15 +661,14 @@ def main():
     units = B * win if win else B                   # CPIs (windows) per GPU per step
     # contiguous shard of the stream per rank (weak scaling): seed = 1000 + config id + first
     # unit index; window mode also holds the look-ahead frame of its last pair (halo)
-    cfg_id = int(args.config[1:])
-    lo, hi = shard.weak_shard(B, rank)
+    plan = rank_plan(args, rank)
     if win:
-        flo, fhi = shard.window_frames(lo, hi)
-        echo = synth.echo_torch(spec, fhi - flo, seed=1000 + cfg_id + flo, device=dev, half=args.half)
+        flo, fhi = plan["frames"]
+        echo = synth.echo_torch(spec, fhi - flo, seed=plan["seed"], device=dev, half=args.half)
         echo = echo.reshape((1, fhi - flo) + tuple(echo.shape[1:]))
         oshape = (1, B, win, P, R)
     else:
-        echo = synth.echo_torch(spec, B, seed=1000 + cfg_id + lo, device=dev, half=args.half)
+        echo = synth.echo_torch(spec, B, seed=plan["seed"], device=dev, half=args.half)
         oshape = (B, P, R)
     rdm = torch.empty(oshape, dtype=torch.float32, device=dev)
     flag = torch.empty(oshape, dtype=torch.uint8, device=dev) if cfar else None
@@ -558,15 +700,19 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    eng.chain_check()   # a fused launch whose bounded in-kernel wait expired invalidates the run
-    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, device=dev)
+    per_rank = shard.gather_over_ranks(elapsed, dist if world > 1 else None, device=dev)
+    elapsed = max(per_rank)
+    plans = [plan]
+    if world > 1:
+        plans = [None] * world
+        dist.all_gather_object(plans, plan)
 
     # Per-kernel device times, measured separately from the throughput: a short pass on ONE
     # chunk pipeline (rsp_set_streams(1)) with every launch bracketed by HIP events on the
     # stream it runs on, so no two kernels overlap and each kernel's time per step is its own
     # (in the timed region the two pipelines overlap PC of one chunk with MTD of the other).
     kernels = launches = None
-    if not args.no_profile and args.lane_steps > 0 and not args.fused:
+    if not args.no_profile and args.lane_steps > 0:
         eng.set_streams(1)
         eng.profile(True, every=1)
         for _ in range(args.lane_steps):
@@ -574,7 +720,7 @@ def main():
         torch.cuda.synchronize(dev)
         prof = eng.profile_read()
         eng.profile(False)
-        eng.set_streams(args.streams or 2)
+        eng.set_streams(args.streams)    # back to what the timed region used (0 = library default)
         kernels = {k: (ms / args.lane_steps, n // args.lane_steps) for k, (ms, n) in prof.items()}
 
     if rank == 0:
@@ -592,7 +738,9 @@ def main():
         # Headline: the whole chain (SURVEY.md §8d algorithmic bytes per CPI x CPIs/s over one
         # step, the dominant cost being two overlapping kernels); traffic = every kernel's
         # PMC HBM-side bytes of a profiled run / the CPIs it processed.
-        roof = {"bound": "hbm", "kernel": "chain (PC + MTD/Doppler-CFAR + range CFAR, 2 pipelines)",
+        pipes = args.streams or (1 if win else 2)      # the library default: rsp.h rsp_set_streams
+        roof = {"bound": "hbm", "kernel": "chain (PC + MTD/Doppler-CFAR%s, %d pipeline%s)" % (
+                    " + range CFAR" if cfar else "", pipes, "" if pipes == 1 else "s"),
                 "achieved": round(chain_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(chain_gbps / HBM_PEAK_GBPS, 4), "traffic": None, "alg_bytes_per_unit": cpi_bytes,
                 "units_per_launch": units, "avg_launch_us": round(gpu_ms * 1e3 / args.steps, 1),
@@ -636,10 +784,9 @@ def main():
             roof["dominant_ms_per_step"] = round(kernels[dom][0], 3)
         achieved = chain_gbps
         host = host_path(eng, echo, cfar, args) if (args.host_path and world == 1 and not win) else None
-        cpu = None
-        if world == 1:
-            # window mode: the reference runs fun_MTD_produce per window, so its rate is CPIs/s
-            cpu = cpu_baseline(spec, cfar, args.cpu_seconds, unit="window/s" if win else "CPI/s")
+        # rank 0 only (the other ranks wait at the closing barrier); window mode: the reference
+        # runs fun_MTD_produce per window, so its rate is CPIs/s
+        cpu = cpu_baseline(spec, cfar, args.cpu_seconds, unit="window/s" if win else "CPI/s")
         mode = "%s: %d pulses x %d range bins, %s, preset %s, PC->MTD->0v%s" % (
             args.config, P, spec.R,
             ("%d frame pairs x %d windows per GPU per step (sliding window, PC shared by windows)" % (B, win))
@@ -670,7 +817,10 @@ def main():
                        "windows_per_pair": win or None, "preset": args.preset,
                        "input": "c32f16" if args.half else "c64",
                        "prefilter": "fused iSTC + MTI(30)" if args.prefilter else None,
-                       "parallelism": "frame-sharded x%d, no collective" % world},
+                       "parallelism": ("%d ranks sharing device 0 (launcher rehearsal, not a scaling result)" % world
+                                       if args.share_device else "frame-sharded x%d, no collective" % world)},
+            "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank],
+            "shards": plans,
             "hbm_GBps_per_gpu": round(achieved, 1),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "roofline": roof,

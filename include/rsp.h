@@ -179,7 +179,7 @@ const char* rsp_last_error(const rsp_ctx* ctx);
  * look-ahead frame); the default there is at least 16 pairs. */
 int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 
-/* Number of chunk pipelines (1..4; default 2, window mode 1): chunk k runs on the caller's stream or on
+/* Number of chunk pipelines (1..4; 0 = the default: 2, window mode 1): chunk k runs on the caller's stream or on
  * one of n-1 context-owned streams that fork from and join back into it, so consecutive
  * chunks overlap.  Each pipeline owns one PC scratch slot. */
 int rsp_set_streams(rsp_ctx* ctx, int32_t n);
@@ -240,17 +240,11 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
                void* stream);
 
 /* ---- execution strategy ------------------------------------------------------------------ */
-/* Fused chain (default off): where the context's shape has a fused kernel (one beam, no
- * windows, P = 128 with the 1024 + 4096-point v2 segment pair), rsp_pc_mtd_cfar_dev and the
- * host entry points run PC -> MTD -> CFAR of the whole call as ONE persistent launch, with
- * the corner turn through a small ring of scratch CPIs instead of a chunk-sized scratch.
- * enable = 0 selects the chunked two-kernel pipeline.  Results are bit-identical.
- * The in-kernel waits are bounded: _dev results of a fused call are valid only once
- * rsp_chain_check returns RSP_OK (the host-buffer entry points check it themselves). */
-int rsp_set_fused(rsp_ctx* ctx, int32_t enable);
-/* Waits for the context's work and reports whether a fused launch gave up waiting for an
- * item (a bounded in-kernel wait that expired): RSP_ERR_HIP with a message if so. */
-int rsp_chain_check(rsp_ctx* ctx);
+/* Overlap-save split of long matched filters (default on): a segment whose FFT exceeds 8192
+ * points, with no output that wraps, runs as 4096..8192-point overlap-save blocks instead of
+ * one whole-length transform (the same correlation sums; results differ by fp32 rounding).
+ * enable = 0 selects the whole-length transforms. */
+int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable);
 
 /* ---- raw-data ingest --------------------------------------------------- */
 /* One frame of the radar's PRT record stream -> DBF beams, replacing the per-PRT loop of
@@ -359,7 +353,9 @@ int rsp_prefilter_dev(rsp_ctx* ctx, const void* d_in, void* d_out, int64_t P, in
  *   mti_lag > 0: applied to the pulse-compressed rows as the MTD loads them -- pulse
  *       compression is linear per row, so PC(x(m+lag) - x(m)) = PC(x(m+lag)) - PC(x(m)) --
  *       over the pulses of each CPI (each window in window mode), zero for its last lag rows.
- * gain == NULL and mti_lag == 0 switch the fused pre-filters off. */
+ * gain == NULL and mti_lag == 0 switch the fused pre-filters off.
+ * rsp_pc_dev (pulse compression alone) applies the gain but not MTI, which lives in the MTD
+ * stage: its rows are PC(gain .* x). */
 int rsp_set_prefilter(rsp_ctx* ctx, const float* gain /* nullable, host [R] */, int32_t mti_lag);
 
 /* ---- diagnostics ---------------------------------------------------------------------- */
@@ -367,10 +363,9 @@ int rsp_set_prefilter(rsp_ctx* ctx, const float* gain /* nullable, host [R] */, 
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1
  * every N-th launch (sampling: each event pair costs the stream a few microseconds),
  * 0 stops.  Any call resets the counters.
- * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V, RSP_K_CHAIN (the fused
- * one-launch chain). */
-#define RSP_NKERNELS 5
-enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3, RSP_K_CHAIN = 4 };
+ * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V. */
+#define RSP_NKERNELS 4
+enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3 };
 int rsp_profile(rsp_ctx* ctx, int32_t enable);
 /* Waits for the recorded events; ms[k] = summed device time, launches[k] = launch count. */
 int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches);

@@ -36,8 +36,8 @@ struct rsp_ctx {
     hipStream_t stream = nullptr;
     rsp::PcArgs pc{};
     bool pc_v2 = false;                 // per-segment specialised kernels (pc_mf_kernel)
-    bool pc_ols_off = false;            // RSP_PC_OLS=0 at create: no overlap-save split (A/B, tests)
-    int pc_ols_min = 8192;              // split segments longer than this (RSP_PC_OLS_MIN at create)
+    int pc_ols_min = 8192;              // overlap-save split of segments longer than this
+    std::vector<rsp::PcMfArgs> pc_mf_whole, pc_mf_split;   // per MF segment, for rsp_set_pc_split
     std::vector<rsp::PcMfArgs> pc_mf;   // one launch per matched-filter segment
     rsp::MtdArgs mtd{};
     int64_t V = 0;                      // Doppler rows (rsp_params.mtd_nfft or P)
@@ -59,8 +59,6 @@ struct rsp_ctx {
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
     DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
-    bool fused = false;                 // one-launch chain where the shape has one (rsp_set_fused)
-    DevBuf chain_ctl;                   // fused chain: queue heads, stage counters, timeout word
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
     // diagnostics (rsp_profile): HIP event pairs around each kernel launch
     struct Ev {
@@ -266,7 +264,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
-                      &ctx->chain_ctl, &ctx->meas_band};
+                      &ctx->meas_band};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -336,8 +334,6 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     rsp_ctx* ctx = new rsp_ctx();
     ctx->device = device;
     ctx->p = p;
-    if (const char* ols = std::getenv("RSP_PC_OLS")) ctx->pc_ols_off = std::atoi(ols) == 0;
-    if (const char* olm = std::getenv("RSP_PC_OLS_MIN")) ctx->pc_ols_min = std::atoi(olm) > 0 ? std::atoi(olm) : 8192;
     for (int s = 0; s < RSP_MAX_SEG; ++s) ctx->p.seg[s].coef_re = ctx->p.seg[s].coef_im = nullptr;
     auto bail = [&](int rc) {
         g_err = ctx->err;
@@ -462,14 +458,20 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
             } else if (!rsp::pc_mf_supported(a.mf.nfft, 0)) {
                 ok = false;
             }
-            if (ok && !ctx->pc_ols_off) {
+            ctx->pc_mf_whole.push_back(a);
+            if (ok) {
                 const int rc = pc_overlap_save(ctx, p.seg[s], a);
                 if (rc) return bail(rc);
             }
+            ctx->pc_mf_split.push_back(a);
             ctx->pc_mf.push_back(a);
         }
         ctx->pc_v2 = ok;
-        if (!ok) ctx->pc_mf.clear();
+        if (!ok) {
+            ctx->pc_mf.clear();
+            ctx->pc_mf_whole.clear();
+            ctx->pc_mf_split.clear();
+        }
     }
 
     // ---- MTD
@@ -650,8 +652,8 @@ int rsp_create_legacy(rsp_ctx** out, int device, int64_t P, int64_t R, const dou
 
 int rsp_set_streams(rsp_ctx* ctx, int32_t n) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_streams: null ctx");
-    if (n < 1 || n > 4) return fail(ctx, RSP_ERR_ARG, "rsp_set_streams: n must be 1..4");
-    ctx->nstreams = n;
+    if (n < 0 || n > 4) return fail(ctx, RSP_ERR_ARG, "rsp_set_streams: n must be 0..4");
+    ctx->nstreams = n;   // 0: the mode-dependent default
     return RSP_OK;
 }
 
@@ -845,6 +847,18 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
     return RSP_OK;
 }
 
+int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_pc_split: null ctx");
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "rsp_set_pc_split: CFAR-only context");
+    const std::vector<rsp::PcMfArgs>& src = enable ? ctx->pc_mf_split : ctx->pc_mf_whole;
+    for (size_t i = 0; i < ctx->pc_mf.size() && i < src.size(); ++i) {
+        const float* gain = ctx->pc_mf[i].gain;   // the fused pre-filter stays as set
+        ctx->pc_mf[i] = src[i];
+        ctx->pc_mf[i].gain = gain;
+    }
+    return RSP_OK;
+}
+
 int rsp_set_prefilter(rsp_ctx* ctx, const float* gain, int32_t mti_lag) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_prefilter: null ctx");
     if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "rsp_set_prefilter: CFAR-only context");
@@ -866,90 +880,6 @@ int rsp_set_prefilter(rsp_ctx* ctx, const float* gain, int32_t mti_lag) {
     return RSP_OK;
 }
 
-int rsp_set_fused(rsp_ctx* ctx, int32_t enable) {
-    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_fused: null ctx");
-    ctx->fused = enable != 0;
-    return RSP_OK;
-}
-
-int rsp_chain_check(rsp_ctx* ctx) {
-    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_chain_check: null ctx");
-    if (!ctx->chain_ctl.p) return RSP_OK;
-    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
-    HIP_TRY(ctx, hipDeviceSynchronize());
-    uint32_t tmo = 0;
-    HIP_TRY(ctx, hipMemcpy(&tmo, (uint32_t*)ctx->chain_ctl.p + (rsp::kChainCtlLines - 1) * rsp::kChainLine,
-                           sizeof(tmo), hipMemcpyDeviceToHost));
-    if (tmo) return fail(ctx, RSP_ERR_HIP, "fused chain: an in-kernel wait expired (results invalid)");
-    return RSP_OK;
-}
-
-// Whether the call can run as one fused launch (chain_kernel's shapes).
-static bool fused_ok(const rsp_ctx* ctx, int32_t dtype, int win, bool pc_input, const float* d_diff,
-                     const rsp::MtdArgs& m) {
-    if (!ctx->fused || pc_input || win > 0 || d_diff || ctx->beams != 1) return false;
-    if (dtype != RSP_C64 && dtype != RSP_C32F16) return false;
-    const int64_t P = ctx->p.P;
-    if (ctx->V != P || m.bnf != 0 || m.pin != P || !ctx->pc_v2 || ctx->pc_mf.size() != 2) return false;
-    if (!rsp::chain_supported((int)P, ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft, m.cv.ref)) return false;
-    const int W = rsp::chain_tile_width((int)P);
-    if (W <= 0 || m.shift % (int)(P / 16) != 0) return false;   // fftshift as a row rotation (G = P/16)
-    if (m.cv.enabled && m.cv.save + m.cv.ref + 2 > 32) return false;
-    return (uint64_t)P * ctx->p.R_out * 8 < 0x80000000ull;
-}
-
-// PC -> MTD -> CFAR of `ncpi` CPIs as one chain_kernel launch (rsp_internal.h ChainArgs).
-static int run_fused(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncpi, const rsp::MtdArgs& m,
-                     const rsp::CfarRArgs& cr, bool cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                     hipStream_t s) {
-    constexpr int NQ = rsp::kChainQueues, S = rsp::kChainSlots;
-    const int64_t P = ctx->p.P, Ro = ctx->p.R_out;
-    const size_t plane = (size_t)P * Ro;
-    if (ncpi > 0x7fffffff / 2) return fail(ctx, RSP_ERR_UNSUPPORTED, "fused chain: batch too large");
-    rsp::ChainArgs a{};
-    a.a1 = ctx->pc_mf[0];
-    a.a2 = ctx->pc_mf[1];
-    a.a1.rows = a.a2.rows = (int)P;
-    a.m = m;
-    a.m.rflag = cfar ? cr.rflag : 0;
-    a.m.flag_zero = 0;   // in-launch hand-off: the flag plane is memset before the launch
-    a.cr = cr;
-    a.echo = d_echo;
-    a.ncpi = (int)ncpi;
-    const int W = rsp::chain_tile_width((int)P);
-    const int64_t nm = (Ro + W - 1) / W;
-    int rc = ensure(ctx, ctx->scratch_pc, (size_t)NQ * S * plane * sizeof(float2));
-    if (rc) return rc;
-    a.scratch = (float2*)ctx->scratch_pc.p;
-    a.rdm_ring = d_rdm == nullptr;
-    if (a.rdm_ring) {
-        rc = ensure(ctx, ctx->tmp_rdm, (size_t)NQ * S * plane * sizeof(float));
-        if (rc) return rc;
-        a.rdm = (float*)ctx->tmp_rdm.p;
-    } else {
-        a.rdm = d_rdm;
-    }
-    a.flag = cfar ? d_flag : nullptr;
-    a.flagV = cfar ? d_flagV : nullptr;
-    if (cfar && cr.rflag) {
-        rc = ensure(ctx, ctx->hit_list, (size_t)NQ * S * nm * W * P * sizeof(uint32_t));
-        if (rc) return rc;
-        rc = ensure(ctx, ctx->hit_ctr, (size_t)NQ * S * nm * sizeof(uint32_t));
-        if (rc) return rc;
-        a.hits = (uint32_t*)ctx->hit_list.p;
-        a.hit_count = (uint32_t*)ctx->hit_ctr.p;
-    }
-    const size_t ctl_bytes = (size_t)rsp::kChainCtlLines * rsp::kChainLine * sizeof(uint32_t);
-    rc = ensure(ctx, ctx->chain_ctl, ctl_bytes);
-    if (rc) return rc;
-    a.ctl = (uint32_t*)ctx->chain_ctl.p;
-    HIP_TRY(ctx, hipMemsetAsync(a.ctl, 0, ctl_bytes, s));
-    if (cfar && cr.rflag)   // background of the flag output; the range items write the 1s
-        HIP_TRY(ctx, hipMemsetAsync(d_flag, 0, (size_t)ncpi * plane, s));
-    HIP_TRY(ctx, timed(ctx, RSP_K_CHAIN, s, [&] { return rsp::launch_chain(dtype, a, s); }));
-    return RSP_OK;
-}
-
 // The chain over `units` on stream s.  win == 0: a unit is one CPI ([P][R] input rows).
 // win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
 // frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
@@ -967,8 +897,6 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     } else {
         m.cv.enabled = 0;
     }
-    if (fused_ok(ctx, dtype, win, pc_input, d_diff, m))
-        return run_fused(ctx, d_echo, dtype, units, m, cr, cfar != nullptr, d_rdm, d_flag, d_flagV, s);
     const int64_t ocpi = win > 0 ? win : 1;               // output CPIs per unit
     m.nwin = win;
     for (int i = 0; i < win; ++i) m.win_start[i] = (int)mround((double)i * P / win);
@@ -979,8 +907,15 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     const int nsd = ctx->nstreams > 0 ? ctx->nstreams : (win > 0 ? 1 : 2);
     if (win > 0) {
         cu = cu / ocpi;
-        if (ctx->chunk > 0) cu = cu > 0 ? cu : 1;          // explicit chunk (rsp_set_chunk): as asked
-        else if (cu < 16) cu = 16;
+        if (ctx->chunk > 0) {
+            cu = cu > 0 ? cu : 1;                          // explicit chunk (rsp_set_chunk): as asked
+        } else if (cu < 16) {
+            // at least 16 pairs, but never more cells per chunk slot than the 32-bit hit
+            // indices address (down to the old minimum and below for the largest windows)
+            const int64_t fit = (int64_t)(0xffffffffull / ((uint64_t)ocpi * (uint64_t)V * (uint64_t)Ro));
+            cu = 16 < fit ? 16 : (fit > cu ? fit : cu);
+            if (cu < 1) cu = 1;
+        }
     }
     if (cu > units) cu = units;
     const int64_t nchunks = (units + cu - 1) / cu;
@@ -1430,7 +1365,6 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
             return rc;
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->fused) return rsp_chain_check(ctx);   // a fused launch whose bounded wait expired is an error
     return RSP_OK;
 }
 

@@ -174,42 +174,6 @@ struct IngestArgs {
 hipError_t launch_ingest_ddc(const uint8_t* stream, int64_t nbytes, const IngestArgs& a, const float2* dbf,
                              float2* out, uint16_t* servo, int32_t* status, hipStream_t s);
 
-// The fused chain: PC -> MTD (+Doppler CFAR) -> range CFAR of a whole call in ONE launch
-// (chain_kernel).  CPI c belongs to work queue c % 8; queue h is a sequence of segments, and
-// segment s holds [PC items of the queue's CPI s][MTD tiles of CPI s-D][range-CFAR items of
-// CPI s-D-1].  Queue-local CPI j uses ring slot j % S of the PC scratch, of the hit lists
-// and (internal RDM) of the RDM.  Workgroups claim items in order from their queue's head
-// (claiming the next one while working on the current one), then steal from the other
-// queues.  Every wait is on an item claimed earlier, so the smallest unfinished item never
-// waits: progress needs no co-residency.
-constexpr int kChainQueues = 8;
-constexpr int kChainSlots = 3;   // S
-constexpr int kChainLag = 1;     // D
-constexpr int kChainLine = 32;   // uint32 words per control line (128 B)
-// control block (zeroed every call): heads at line h; counters of (h, slot) at line
-// 8 + h*S + slot, words 0 = PC items done, 1 = MTD tiles done, 2 = range items done; the
-// last line holds the timeout word
-constexpr int kChainCtlLines = kChainQueues + kChainQueues * kChainSlots + 1;
-
-struct ChainArgs {
-    PcMfArgs a1, a2;        // short segment (FIR + N1-point MF) and long segment (N2 MF), rows = P
-    MtdArgs m;              // MTD + Doppler CFAR (pc / hits / rdm pointers come from below)
-    CfarRArgs cr;           // range CFAR (rflag)
-    const void* echo;       // [ncpi][P][R]
-    float2* scratch;        // [8][S][P][R_out]
-    float* rdm;             // [ncpi][P][R_out], or the ring [8][S][P][R_out] when rdm_ring
-    int rdm_ring;
-    uint8_t* flag;          // [ncpi][P][R_out] (zeroed when rflag), or null: no CFAR
-    uint8_t* flagV;         // [ncpi][P][R_out] or null
-    uint32_t* hits;         // [8][S][nm][W*P]
-    uint32_t* hit_count;    // [8][S][nm]
-    uint32_t* ctl;          // kChainCtlLines * kChainLine words
-    int ncpi;
-    int nl, nsh, nm, nh;    // items per CPI: long rows, short-row groups, MTD tiles, range items
-    int grid;
-};
-
-
 bool mtd_size_supported(int P, int beams = 1);
 bool pc_nfft_supported(int n);
 size_t pc_lds_bytes(int max_nfft);
@@ -248,11 +212,6 @@ hipError_t launch_ingest(const void* in, int dtype, int layout, float2* out, int
 // [batch][A][B] -> [batch][B][A] for 4-byte and 1-byte elements.
 hipError_t launch_transpose_f32(const float* in, float* out, int64_t batch, int A, int B,
                                 hipStream_t s);
-// The fused chain: supported(P, n1, n2) says whether chain_kernel is built for the shape;
-// launch_chain fills a.nl/nsh/nm/nh/grid and launches (a.ctl zeroed by the caller).
-bool chain_supported(int P, int n1, int n2, int ref);
-int chain_tile_width(int P);
-hipError_t launch_chain(int dtype, ChainArgs& a, hipStream_t s);
 hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, int A, int B,
                                hipStream_t s);
 

@@ -176,7 +176,7 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
 template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t,
-                                        const float* __restrict__ gain) {
+                                        const float* __restrict__ gain, bool st_ok = true) {
     float2* s2 = reinterpret_cast<float2*>(stage);
     const int kp = g.ntaps4 - 1;
     const int len = g.out_len;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             w[5] = w[1];
             w[4] = w[0];
         }
-        if (valid) {
+        if (valid && st_ok) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int m = m0 + i;
@@ -276,7 +276,16 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         sub = __builtin_amdgcn_readfirstlane(sub);
     }
     const bool valid = row < a.rows;
+#ifdef RSP_DIAG_PC_L2IN   // dev-only diagnostic build (tools/build_variant.sh): rows read 64 L2-resident inputs
+    const TIn* x = echo + (size_t)(row & 63) * a.R;
+#else
     const TIn* x = echo + (size_t)row * a.R;
+#endif
+#ifdef RSP_DIAG_PC_NOSTORE   // dev-only diagnostic build: every output store range-checked away
+    const bool st_ok = valid && a.rows < 0;
+#else
+    const bool st_ok = valid;
+#endif
     float2* y = out + (size_t)row * a.R_out;
     int in_start = a.mf.in_start, in_len = a.mf.in_len;
     int out_start = a.mf.out_start, out_len = a.mf.out_len;
@@ -326,9 +335,11 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
                 for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) st_c<SA>(y + c, make_float2(0.f, 0.f));
-        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t, a.gain);
+        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t, a.gain, st_ok);
     }
+#ifndef RSP_DIAG_PC_NOFFT   // dev-only diagnostic build: load, spectrum multiply, store (no FFTs)
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
+#endif
     if constexpr (kEarly) {
 #pragma unroll
         for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hs[m]);   // conj(X.*H), 1/N in H
@@ -343,12 +354,14 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
         }
     }
+#ifndef RSP_DIAG_PC_NOFFT
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
+#endif
     if constexpr (kUniform) {
-        const auto yr = buf_rsrc(y + out_start, valid ? (uint32_t)out_len * 8u : 0u);
+        const auto yr = buf_rsrc(y + out_start, st_ok ? (uint32_t)out_len * 8u : 0u);
 #pragma unroll
         for (int m = 0; m < E; ++m) buf_st_f2a<SA>(cconj(u[m]), yr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
-    } else if (valid) {
+    } else if (st_ok) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int i = t + G * m;
@@ -371,7 +384,10 @@ struct PairCfg {
 // Single segment (N2 == 0) or two independent segments in one launch: blocks
 // [0, nblk2) run segment 2 (the long one, first for a short tail), the rest segment 1.
 template <typename TIn, int N1, int N2>
-__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_kernel(
+#ifndef RSP_DIAG_PC_WAVES   // dev-only diagnostic build: minimum waves per SIMD of the PC kernel
+#define RSP_DIAG_PC_WAVES 2
+#endif
+__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_DIAG_PC_WAVES) void pc_mf_kernel(
     const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
@@ -395,25 +411,6 @@ __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), 2) void pc_mf_ker
     pc_row<TIn, N1, G, 0, G == 64>(echo, out, a1, u / ns, t, lds + grp * PcCfg<N1>::SLOT, u % ns);
 }
 
-
-static int device_cus(int dev) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    return cus;
-}
-
-// Resident workgroups of a persistent kernel on the current device (once per device).
-static hipError_t resident_grid(LaunchOnce& once, const void* kernel, int threads, size_t lds, int* resident) {
-    return launch_once(once, resident, [&](int dev, int* out) {
-        hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        int per_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds);
-        if (e != hipSuccess) return e;
-        *out = (per_cu > 0 ? per_cu : 1) * device_cus(dev);
-        return hipSuccess;
-    });
-}
 
 // Dynamic-LDS attribute of a kernel (once per device).
 static hipError_t lds_attr(LaunchOnce& once, const void* kernel, size_t lds) {
@@ -446,6 +443,14 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     const int u2 = a2 ? a2->rows * (a2->nsub > 1 ? a2->nsub : 1) : 0;
     const int nblk2 = N2 ? (u2 + PC::RPB2 - 1) / PC::RPB2 : 0;
     dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
+#ifdef RSP_DIAG_PC_LDS_EXTRA   // dev-only diagnostic build: extra dynamic LDS to cap workgroups per CU
+    static LaunchOnce once_x;
+    e = lds_attr(once_x, (const void*)pc_mf_kernel<TIn, N1, N2>, PC::lds + RSP_DIAG_PC_LDS_EXTRA);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds + RSP_DIAG_PC_LDS_EXTRA, s, echo, out, a1,
+                       a2 ? *a2 : a1, nblk2);
+    return hipGetLastError();
+#endif
     hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds, s, echo, out, a1,
                        a2 ? *a2 : a1, nblk2);
     return hipGetLastError();
@@ -1783,221 +1788,6 @@ hipError_t launch_transpose_f32(const float* in, float* out, int64_t batch, int 
 hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, int A, int B,
                                hipStream_t s) {
     return launch_transpose_t(in, out, batch, A, B, s);
-}
-
-// ================================================================== fused chain (one launch)
-// PC -> MTD (+Doppler CFAR) -> range CFAR of a whole call in one persistent launch; the work
-// queues and their ordering are described with ChainArgs (rsp_internal.h).  Hand-offs
-// between the stages cross workgroups (and XCDs) inside the launch, so they follow the
-// write-through protocol of rsp_buf.h: the PC scratch, the RDM and the hit lists are stored
-// `sc1`, every storing wave drains vmcnt before its workgroup's one counter add, and every
-// load of handed-off bytes is an `sc1` load issued after thread 0 saw the counter.  The
-// corner turn's scratch is a ring of kChainSlots CPIs per queue (96 MiB at 128 x 4096), so it
-// is re-read from the Infinity Cache a few CPIs after it was written, instead of from HBM.
-__device__ __forceinline__ uint32_t* chain_head(uint32_t* ctl, int h) { return ctl + h * kChainLine; }
-__device__ __forceinline__ uint32_t* chain_ctr(uint32_t* ctl, int h, int slot) {
-    return ctl + (kChainQueues + h * kChainSlots + slot) * kChainLine;
-}
-__device__ __forceinline__ uint32_t chain_claim(uint32_t* ctl, int h) {
-    return __hip_atomic_fetch_add((gu32*)chain_head(ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Thread 0: wait until *p >= target (relaxed agent-scope polls with s_sleep between).  A
-// wait that lasts 0.5 s sets the timeout word, and once it is set no wait blocks: the launch
-// then completes with wrong data (reported by rsp_chain_check) instead of hanging the GPU.
-__device__ __forceinline__ void chain_wait(uint32_t* p, uint32_t target, uint32_t* tmo) {
-    if (__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s of the 100 MHz clock
-            __hip_atomic_fetch_or((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-    }
-}
-
-// Every wave drains its stores, then thread 0 publishes the workgroup's item.
-__device__ __forceinline__ void chain_signal(uint32_t* p) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int N1, int N2, int P>
-struct ChainCfg {
-    using PC = PairCfg<N1, N2>;
-    using MC = MtdCfg<P>;
-    static constexpr size_t main = PC::lds > MC::lds ? PC::lds : MC::lds;
-    static constexpr size_t lds = ((main + 15) & ~(size_t)15) + 16;   // + control words
-};
-
-template <typename TIn, int N1, int N2, int P, int REF>
-__device__ __forceinline__ void chain_item(const ChainArgs& a, int h, uint32_t q, unsigned char* smem,
-                                           uint32_t* s_hits, uint32_t* tmo) {
-    constexpr int S = kChainSlots, D = kChainLag;
-    using PC = PairCfg<N1, N2>;
-    using MC = MtdCfg<P>;
-    const int tid = threadIdx.x;
-    const int npc = a.nl + a.nsh;
-    const int ips = npc + a.nm + a.nh;
-    const int seg = (int)(q / (uint32_t)ips), k = (int)(q % (uint32_t)ips);
-    int j, kind, idx;
-    if (k < npc) { j = seg; kind = 0; idx = k; }
-    else if (k < npc + a.nm) { j = seg - D; kind = 1; idx = k - npc; }
-    else { j = seg - D - 1; kind = 2; idx = k - npc - a.nm; }
-    const int c = h + kChainQueues * j;
-    if (j < 0 || c >= a.ncpi) return;
-    const int slot = j % S;
-    const uint32_t gen = (uint32_t)(j / S);
-    uint32_t* ctr = chain_ctr(a.ctl, h, slot);
-    const size_t R = (size_t)a.a2.R, Ro = (size_t)a.a2.R_out;
-    const size_t plane = (size_t)P * Ro;
-    const size_t ring = (size_t)(h * S + slot);
-    float2* pcs = a.scratch + ring * P * Ro;
-    float* rdm = a.rdm_ring ? a.rdm + ring * plane : a.rdm + (size_t)c * plane;
-    constexpr uint32_t region = (uint32_t)(MC::W * P);
-    if (kind == 0) {   // one PC item: a long-segment row, or PC::RPB1 short-segment rows
-        if (tid == 0 && gen > 0) chain_wait(ctr + 1, gen * (uint32_t)a.nm, tmo);   // slot free
-        __syncthreads();
-        const TIn* ein = (const TIn*)a.echo + (size_t)c * P * R;
-        if (idx < a.nl) {
-            pc_row<TIn, N2, kBlock, kSc1>(ein, pcs, a.a2, idx, tid, reinterpret_cast<float2*>(smem));
-        } else {
-            constexpr int G1 = PcCfg<N1>::G;
-            const int grp = tid / G1;
-            pc_row<TIn, N1, G1, kSc1>(ein, pcs, a.a1, (idx - a.nl) * PC::RPB1 + grp, tid % G1,
-                                      reinterpret_cast<float2*>(smem) + grp * PcCfg<N1>::SLOT);
-        }
-        chain_signal(ctr + 0);
-    } else if (kind == 1) {   // one MTD tile (+ Doppler CFAR, hit list)
-        if (tid == 0) {
-            chain_wait(ctr + 0, (gen + 1) * (uint32_t)npc, tmo);                     // CPI's PC
-            if (a.nh > 0 && gen > 0) chain_wait(ctr + 2, gen * (uint32_t)a.nh, tmo);  // hit slot free
-        }
-        __syncthreads();
-        MtdTile T;
-        T.pc = pcs;
-        T.rdm = rdm;
-        T.diff = nullptr;
-        T.flagV = a.flagV ? a.flagV + (size_t)c * plane : nullptr;
-        T.flag = a.flag ? a.flag + (size_t)c * plane : nullptr;
-        T.hits = a.nh > 0 ? a.hits + (ring * a.nm + idx) * region : nullptr;
-        T.hit_count = a.nh > 0 ? a.hit_count + ring * a.nm + idx : nullptr;
-        T.cell_base = 0;
-        T.bx = idx;
-        mtd_tile<P, REF, 1, kSc1, kSc1>(T, a.m, smem, s_hits);
-        chain_signal(ctr + 1);
-    } else {   // range CFAR at the Doppler hits of a run of the CPI's tiles (one wave per tile)
-        if (tid == 0) chain_wait(ctr + 1, (gen + 1) * (uint32_t)a.nm, tmo);
-        __syncthreads();
-        const int lane = tid & 63, w = tid >> 6;
-        const uint32_t* hl = a.hits + ring * a.nm * region;
-        const uint32_t* hc = a.hit_count + ring * a.nm;
-        uint8_t* fl = a.flag + (size_t)c * plane;
-        const int per = (a.nm + a.nh - 1) / a.nh;
-        const int r0 = idx * per, r1 = r0 + per < a.nm ? r0 + per : a.nm;
-        const bool ref57 = a.cr.ref == 5 && a.cr.save == 7;
-        for (int rg = r0 + w; rg < r1; rg += kBlock / 64) {
-            if (ref57) cfar_hit_region<5, 7, kSc1>(rdm, fl, hl, hc, rg, region, a.cr, lane);
-            else cfar_hit_region<0, 0, kSc1>(rdm, fl, hl, hc, rg, region, a.cr, lane);
-        }
-        chain_signal(ctr + 2);
-    }
-}
-
-template <typename TIn, int N1, int N2, int P, int REF>
-__global__ __launch_bounds__(kBlock, 2) void chain_kernel(ChainArgs a) {
-    using CC = ChainCfg<N1, N2, P>;
-    static_assert(CC::PC::T == kBlock && PcCfg<N2>::G == kBlock, "one long-segment row per workgroup");
-    static_assert(CC::MC::W * CC::MC::G == kBlock, "MTD tile shape");
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* sw = reinterpret_cast<uint32_t*>(smem + ((CC::main + 15) & ~(size_t)15));   // [0] item, [1] hits
-    const int tid = threadIdx.x;
-    const int ips = a.nl + a.nsh + a.nm + a.nh;
-    const int extra = a.nh > 0 ? kChainLag + 1 : kChainLag;
-    uint32_t* tmo = a.ctl + (kChainCtlLines - 1) * kChainLine;
-    int h = (int)(blockIdx.x % kChainQueues);   // home queue; placement changes speed only
-    auto total = [&](int qh) -> uint32_t {
-        const int J = a.ncpi > qh ? (a.ncpi - qh + kChainQueues - 1) / kChainQueues : 0;
-        return J > 0 ? (uint32_t)(J + extra) * (uint32_t)ips : 0u;
-    };
-    if (tid == 0) sw[0] = chain_claim(a.ctl, h);
-    __syncthreads();
-    // the item number is wave-uniform: readfirstlane keeps everything derived from it in SGPRs
-    // (buffer resources built from a VGPR value would need waterfall loops)
-    uint32_t q = __builtin_amdgcn_readfirstlane(sw[0]);
-    int tried = 1;
-    for (;;) {
-        __syncthreads();   // every thread has read sw[0]
-        if (q >= total(h)) {   // queue drained: steal from the next one
-            if (tried == kChainQueues) break;
-            ++tried;
-            h = (h + 1) % kChainQueues;
-            if (tid == 0) sw[0] = chain_claim(a.ctl, h);
-            __syncthreads();
-            q = __builtin_amdgcn_readfirstlane(sw[0]);
-            continue;
-        }
-        uint32_t nxt = 0;
-        if (tid == 0) nxt = chain_claim(a.ctl, h);   // claim ahead: its latency overlaps the item
-        // Re-read the arguments inside every item: an opaque copy of the kernarg pointer stops
-        // the compiler from hoisting every field any item type uses into SGPRs for the whole
-        // loop (hundreds of SGPR spills otherwise).
-        // (the kernel's only argument sits at offset 0 of the kernarg segment)
-        typedef const __attribute__((address_space(4))) ChainArgs ChainArgsK;
-        const ChainArgsK* ap = (const ChainArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ap));
-        chain_item<TIn, N1, N2, P, REF>(*(const ChainArgs*)ap, h, q, smem, sw + 1, tmo);
-        __syncthreads();
-        if (tid == 0) sw[0] = nxt;
-        __syncthreads();
-        q = __builtin_amdgcn_readfirstlane(sw[0]);
-    }
-}
-
-template <typename TIn, int N1, int N2, int P, int REF>
-static hipError_t launch_chain_t(ChainArgs& a, hipStream_t s) {
-    using CC = ChainCfg<N1, N2, P>;
-    static LaunchOnce once;
-    int resident = 0;
-    hipError_t e = resident_grid(once, (const void*)chain_kernel<TIn, N1, N2, P, REF>, kBlock, CC::lds, &resident);
-    if (e != hipSuccess) return e;
-    a.nl = P;
-    a.nsh = (P + CC::PC::RPB1 - 1) / CC::PC::RPB1;
-    a.nm = (a.a2.R_out + CC::MC::W - 1) / CC::MC::W;
-    a.nh = (a.flag && a.cr.rflag) ? (a.nm + 31) / 32 : 0;
-    const int64_t items = (int64_t)a.ncpi * (a.nl + a.nsh + a.nm + a.nh);
-    a.grid = items < resident ? (int)items : resident;
-    if (a.grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((chain_kernel<TIn, N1, N2, P, REF>), dim3((unsigned)a.grid), dim3(kBlock), CC::lds, s, a);
-    return hipGetLastError();
-}
-
-bool chain_supported(int P, int n1, int n2, int ref) {
-    (void)ref;
-    return PairCfg<1024, 4096>::T == kBlock && P == 128 && n1 == 1024 && n2 == 4096;
-}
-
-int chain_tile_width(int P) { return P == 128 ? MtdCfg<128>::W : 0; }
-
-template <typename TIn>
-static hipError_t launch_chain_d(ChainArgs& a, hipStream_t s) {
-    const bool ref5 = a.m.cv.enabled && a.m.cv.ref == 5;
-    if constexpr (PairCfg<1024, 4096>::T == kBlock) {   // (a PC build with other row widths has no chain)
-        if (a.m.P == 128 && a.a1.mf.nfft == 1024 && a.a2.mf.nfft == 4096 && a.a1.nsub <= 1 && a.a2.nsub <= 1)
-            return ref5 ? launch_chain_t<TIn, 1024, 4096, 128, 5>(a, s) : launch_chain_t<TIn, 1024, 4096, 128, 0>(a, s);
-    }
-    (void)ref5;
-    return hipErrorNotSupported;
-}
-
-hipError_t launch_chain(int dtype, ChainArgs& a, hipStream_t s) {
-    if (a.ncpi <= 0) return hipSuccess;
-    if (dtype == RSP_C64) return launch_chain_d<float2>(a, s);
-    if (dtype == RSP_C32F16) return launch_chain_d<__half2>(a, s);
-    return hipErrorInvalidValue;
 }
 
 }  // namespace rsp

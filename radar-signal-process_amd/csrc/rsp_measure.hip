@@ -562,14 +562,18 @@ hipError_t launch_e(const float* sum, const float* diff, const uint8_t* flag, in
 
 }  // namespace
 
-// Opt-in (RSP_MEASURE_BANDS=N > 1, A/B): N bands per CPI for batches below the CU count.
+// Dev-only build (-DRSP_DEV_MEASURE_BANDS=N > 1, tools/build_variant.sh): N bands per CPI for
+// batches below the CU count.
 // Measured slower than one workgroup per CPI at every batch tried (2048 x 512, ~1044 hits:
 // batch 1 113 vs 64 us, batch 8 84 vs 65 us, batch 64 100 vs 79 us per call): its three
 // launches each cost more than the single workgroup's whole flag scan (band_scan alone 50 us
 // of dependent loads in one workgroup).  Bit-exact against the oracle when enabled.
 int measure_bands(int V, int batch) {
-    static const char* env = getenv("RSP_MEASURE_BANDS");
-    const int want = env ? atoi(env) : 1;
+#ifdef RSP_DEV_MEASURE_BANDS
+    const int want = RSP_DEV_MEASURE_BANDS;
+#else
+    const int want = 1;
+#endif
     if (want <= 1 || batch >= 128) return 1;
     const int max_nb = (V + 31) / 32;                      // bands of at least 32 rows
     return want < max_nb ? want : max_nb;

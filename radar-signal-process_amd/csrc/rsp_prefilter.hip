@@ -118,7 +118,11 @@ hipError_t launch_prefilter(const float2* in, float2* out, const float* gain, in
     const float4* i4 = reinterpret_cast<const float4*>(in);
     float4* o4 = reinterpret_cast<float4*>(out);
     const float2* g2 = reinterpret_cast<const float2*>(gain);
-    static const bool rowwise = getenv("RSP_MTI_ROWWISE") != nullptr;   // A/B: the row-parallel form
+#ifdef RSP_DEV_MTI_ROWWISE   // dev-only build (tools/build_variant.sh): the row-parallel form, measured slower
+    constexpr bool rowwise = true;
+#else
+    constexpr bool rowwise = false;
+#endif
     if (lag > 0 && !rowwise)
         return gain ? launch_chain<true>(i4, o4, g2, P, R / 2, lag, batch, st)
                     : launch_chain<false>(i4, o4, g2, P, R / 2, lag, batch, st);

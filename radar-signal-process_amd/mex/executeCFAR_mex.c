@@ -13,10 +13,20 @@
  */
 #include <string.h>
 
+#include <stdlib.h>
+
 #include "mex.h"
 #include "rsp.h"
 
 static rsp_ctx* g_ctx = NULL;
+
+/* GPU of the shim's context: RSP_MEX_DEVICE (a HIP device index, default 0), read when the
+ * context is created (first call, or a call whose parameters change); setenv('RSP_MEX_DEVICE',
+ * '3') in MATLAB before that call places it on device 3.  One MATLAB process drives one GPU. */
+static int mex_device(void) {
+    const char* d = getenv("RSP_MEX_DEVICE");
+    return d && *d ? atoi(d) : 0;
+}
 
 static void cleanup(void) {
     if (g_ctx) rsp_destroy(g_ctx);
@@ -44,7 +54,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     cf.zero_v_div = 0;
     cf.nseg = 0;
     if (!g_ctx) {
-        if (rsp_create(&g_ctx, 0, NULL) != RSP_OK) {
+        if (rsp_create(&g_ctx, mex_device(), NULL) != RSP_OK) {
             g_ctx = NULL;
             mexErrMsgIdAndTxt("rsp:create", "%s", rsp_last_error(NULL));
         }

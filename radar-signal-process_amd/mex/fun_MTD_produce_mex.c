@@ -30,6 +30,14 @@
 #endif
 
 static rsp_ctx* g_ctx = NULL;
+
+/* GPU of the shim's context: RSP_MEX_DEVICE (a HIP device index, default 0), read when the
+ * context is created (first call, or a call whose parameters change); setenv('RSP_MEX_DEVICE',
+ * '3') in MATLAB before that call places it on device 3.  One MATLAB process drives one GPU. */
+static int mex_device(void) {
+    const char* d = getenv("RSP_MEX_DEVICE");
+    return d && *d ? atoi(d) : 0;
+}
 static double g_key[12];
 
 static void cleanup(void) {
@@ -107,7 +115,7 @@ static int create_legacy(int64_t P, int64_t R, char* err, size_t errn) {
     if (read_npy_c128(path, &re2, &im2, &n2, err, errn) == 0) {
         snprintf(path, sizeof(path), "%s/legacy_pulse3.npy", dir);
         if (read_npy_c128(path, &re3, &im3, &n3, err, errn) == 0) {
-            if (rsp_create_legacy(&g_ctx, 0, P, R, re2, im2, n2, re3, im3, n3) == RSP_OK) rc = 0;
+            if (rsp_create_legacy(&g_ctx, mex_device(), P, R, re2, im2, n2, re3, im3, n3) == RSP_OK) rc = 0;
             else { g_ctx = NULL; snprintf(err, errn, "%s", rsp_last_error(NULL)); }
         }
     }
@@ -139,7 +147,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         char err[512] = "";
         if (nrhs == 2) {
             int64_t point_prt[4] = {R, (int64_t)pp[1], (int64_t)pp[2], (int64_t)pp[3]};
-            if (rsp_create_v2(&g_ctx, 0, P, R, point_prt, fs, B, tao) != RSP_OK) {
+            if (rsp_create_v2(&g_ctx, mex_device(), P, R, point_prt, fs, B, tao) != RSP_OK) {
                 g_ctx = NULL;
                 mexErrMsgIdAndTxt("rsp:create", "%s", rsp_last_error(NULL));
             }

@@ -54,14 +54,16 @@ class Engine:
         self.close()
 
     def set_streams(self, n):
+        """Chunk pipelines 1..4, or 0 for the library's mode-dependent default."""
         capi.check(self.lib.rsp_set_streams(self.ctx, int(n)), self.ctx)
 
     def set_chunk(self, cpis):
         capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)
 
-    def set_fused(self, enable):
-        """One-launch fused chain where the shape has one (1); 0 = chunked pipeline (default)."""
-        capi.check(self.lib.rsp_set_fused(self.ctx, int(enable)), self.ctx)
+    def set_pc_split(self, enable):
+        """Overlap-save blocks for matched filters longer than 8192 points (1, the default) or
+        whole-length transforms (0) -- rsp_set_pc_split."""
+        capi.check(self.lib.rsp_set_pc_split(self.ctx, int(enable)), self.ctx)
 
     def set_prefilter(self, gain=None, mti_lag=0):
         """Fuse iSTC (gain: [R] linear gains, e.g. rsp.prefilter.istc_gain) into pulse
@@ -74,10 +76,6 @@ class Engine:
                 raise ValueError("gain must have R = %d entries" % self.spec.R)
         ptr = g.ctypes.data_as(C.POINTER(C.c_float)) if g is not None else None
         capi.check(self.lib.rsp_set_prefilter(self.ctx, ptr, int(mti_lag)), self.ctx)
-
-    def chain_check(self):
-        """Raise if a fused launch of this context gave up waiting for an item."""
-        capi.check(self.lib.rsp_chain_check(self.ctx), self.ctx)
 
     @property
     def shape(self):

@@ -23,11 +23,28 @@ def window_frames(lo, hi):
     return lo, hi + 1
 
 
+def _coll_device(dist, device):
+    """gloo reduces host tensors; RCCL ("nccl") reduces device tensors."""
+    return "cpu" if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(value, dist=None, device=None):
     """Max of a float over all ranks (identity without an initialised process group)."""
     if dist is None or not dist.is_available() or not dist.is_initialized():
         return float(value)
     import torch
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_coll_device(dist, device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_over_ranks(value, dist=None, device=None):
+    """Every rank's float, in rank order ([value] without an initialised process group)."""
+    if dist is None or not dist.is_available() or not dist.is_initialized():
+        return [float(value)]
+    import torch
+    dev = _coll_device(dist, device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]

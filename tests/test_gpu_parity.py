@@ -64,16 +64,16 @@ def test_pc_parity(torch_cuda, name, P, R):
 
 
 @pytest.mark.parametrize("R", [16384, 12000])
-def test_pc_overlap_save_matches_whole_transform(torch_cuda, monkeypatch, R):
+def test_pc_overlap_save_matches_whole_transform(torch_cuda, R):
     """The 16384-point segment runs as overlap-save blocks of 4096 (pc_overlap_save); the
-    whole-length transform (RSP_PC_OLS=0) must give the same correlation to fp32 rounding,
-    and every column outside the split segment bit-identically."""
+    whole-length transform (rsp_set_pc_split(ctx, 0)) must give the same correlation to fp32
+    rounding, and every column outside the split segment bit-identically."""
     torch = torch_cuda
     P = 16
     outs = []
-    for ols in ("1", "0"):
-        monkeypatch.setenv("RSP_PC_OLS", ols)
+    for ols in (1, 0):
         eng = _engine("v2", P, R)
+        eng.set_pc_split(ols)
         echo = _echo(eng, 1, seed=77)
         d_in = torch.from_numpy(echo).cuda()
         d_pc = torch.empty((1, P, R), dtype=torch.complex64, device="cuda")

@@ -39,14 +39,21 @@ def _windows(frames, win):
     return out
 
 
-@pytest.mark.parametrize("P,R,beams,nf,win,chunk", [(64, 1024, 2, 3, 4, 0), (128, 4096, 1, 2, 4, 0),
-                                                     (64, 1024, 1, 5, 3, 8), (96, 1024, 1, 2, 5, 0)])
-def test_window_bit_exact_vs_sliced_chain(torch_cuda, P, R, beams, nf, win, chunk):
+@pytest.mark.parametrize("P,R,beams,nf,win,chunk,streams,prefilter", [
+    (64, 1024, 2, 3, 4, 0, 0, False), (128, 4096, 1, 2, 4, 0, 0, False), (64, 1024, 1, 5, 3, 8, 0, False),
+    (96, 1024, 1, 2, 5, 0, 0, False),
+    # several chunks on two pipelines (two scratch slots, each chunk with its look-ahead frame)
+    (64, 1024, 1, 7, 4, 8, 2, False), (64, 1024, 2, 5, 3, 3, 2, False),
+    # the fused pre-filters (iSTC gain in PC's load, MTI lag 9 in the MTD's load) in window mode
+    (64, 1024, 1, 4, 4, 0, 0, True), (64, 1024, 1, 5, 4, 8, 2, True)])
+def test_window_bit_exact_vs_sliced_chain(torch_cuda, P, R, beams, nf, win, chunk, streams, prefilter):
     torch = torch_cuda
     from rsp import presets, synth
     from rsp.engine import Engine
     spec = presets.v2(P, R)
-    eng = Engine(spec, device=0, chunk=chunk)
+    eng = Engine(spec, device=0, chunk=chunk, streams=streams)
+    if prefilter:
+        eng.set_prefilter(gain=np.linspace(0.5, 2.0, R).astype(np.float32), mti_lag=9)
     cf = presets.default_cfar(spec)
     frames = synth.echo_numpy(spec, beams * (nf + 1), seed=1004).reshape(beams, nf + 1, P, R)
     d_frames = torch.from_numpy(frames).cuda()

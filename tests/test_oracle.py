@@ -199,3 +199,32 @@ def test_builtins_against_scipy():
     _, gd = sig.group_delay((b, [1.0]), w=512)
     assert abs(np.mean(gd) - 17.0) < 1e-6
     assert ref.grpdelay_round_mean(b) == int(np.floor(np.mean(gd) + 0.5)) == 17
+
+
+@pytest.mark.parametrize("name,P,R", [("legacy", 1536, 1031), ("v2", 332, 3404), ("v2", 256, 8192),
+                                      ("v2", 512, 16384)])
+def test_c_oracle_matches_numpy_oracle_at_checker_sizes(name, P, R):
+    """Guard of the large-shape checker: the C oracle (which checks the GPU at the legacy
+    native 1536 x 1031 CPI, the v2 native 332 x 3404, c4's 256 x 8192 and c5's 512 x 16384)
+    against the loop-faithful numpy oracle on one synthetic CPI of each (SURVEY.md §8d echo),
+    fun_MTD_produce + main_cfar's executeCFAR chain with the preset's default CFAR: RDM within
+    1e-13, flag and flagV planes identical (executeCFAR.m:21-92, fun_Process_MTD.m:27-37)."""
+    from rsp import presets, synth
+    spec = presets.make(name, P, R)
+    echo = synth.echo_numpy(spec, 1, seed=1200 + P).astype(np.complex128)
+    pre = coracle.preset(name, P, R)
+    rc = coracle.pc_mtd(echo, pre)
+    if name == "v2":
+        rn = ref.fun_MTD_produce_v2(echo[0], ref.v2_params(P, R))[None]
+    else:
+        rn = ref.fun_MTD_produce_legacy(echo[0], np.load(DATA + "/legacy_pulse2.npy"),
+                                        np.load(DATA + "/legacy_pulse3.npy"))[None]
+    assert np.linalg.norm(rc - rn) / np.linalg.norm(rn) < 1e-13
+    cf = presets.default_cfar(spec)
+    c = cf.as_dict()
+    c["zero_v_div"] = cf.zero_v_div
+    fc, fvc = coracle.cfar(rn, c, cf.segments)
+    f, fv = ref.main_cfar_chain(rn[0], c, [(a + 1, b) for a, b in cf.segments], cf.zero_v_div)
+    np.testing.assert_array_equal(fc[0], f)
+    np.testing.assert_array_equal(fvc[0], fv)
+    assert f.sum() > 0
