@@ -196,6 +196,17 @@ def cpu_baseline(spec, cfar, seconds, unit="CPI/s"):
             "host": cpus}
 
 
+def hbm_ceiling():
+    """The measured streaming ceiling of this part (profiles/hbm_ceiling.json, written from
+    tools/micro/hbm_ceiling.hip): copy (equal read and write bytes, the chain's mix), read-only,
+    write-only GB/s."""
+    p = os.path.join(ROOT, "profiles", "hbm_ceiling.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
 def pmc_traffic(tag):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if one exists."""
     p = os.path.join(ROOT, "profiles", "pmc_%s.json" % tag)
@@ -746,6 +757,10 @@ def main():
                 "units_per_launch": units, "avg_launch_us": round(gpu_ms * 1e3 / args.steps, 1),
                 "note": "one step = one launch sequence over the batch; achieved = units/s (device events "
                         "around the timed steps) x alg bytes per unit"}
+        ceil = hbm_ceiling()
+        if ceil:
+            roof["ceiling"] = {"copy_GBps": ceil["copy_GBps"], "read_GBps": ceil["read_GBps"],
+                               "write_GBps": ceil["write_GBps"], "source": "profiles/hbm_ceiling.json"}
         if pmc and pmc.get("bytes_per_unit"):
             # per launch like `achieved` (one launch sequence = one step of `units` CPIs/windows)
             roof["traffic"] = int(pmc["bytes_per_unit"] * units)
@@ -753,6 +768,12 @@ def main():
             roof["traffic_per_unit"] = int(pmc["bytes_per_unit"])
             roof["traffic_ratio"] = round(pmc["bytes_per_unit"] / cpi_bytes, 3)
             roof["traffic_source"] = "profiles/pmc_%s.json" % tag
+            if ceil:
+                # the counted L2<->fabric bytes per second of this run against the measured copy
+                # ceiling (Infinity-Cache hits are counted too, so this can exceed 1 in principle)
+                counted_gbps = pmc["bytes_per_unit"] * per_gpu_units_s / 1e9
+                roof["counted_GBps"] = round(counted_gbps, 1)
+                roof["ceiling_frac"] = round(counted_gbps / ceil["copy_GBps"], 4)
         if kernels:
             # each kernel's own compulsory bytes per launch: PC reads the echo and writes the
             # pulse-compressed rows; MTD reads them and writes the RDM and the flag plane
@@ -773,7 +794,13 @@ def main():
                     k["achieved"] = round(ab / (avg_us * 1e3), 1)
                     k["frac"] = round(ab / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
                 if pmc and name in pmc.get("kernels", {}):
-                    k["hbm_bytes_per_launch"] = pmc["kernels"][name].get("hbm_bytes_per_launch")
+                    pk = pmc["kernels"][name]
+                    k["hbm_bytes_per_launch"] = pk.get("hbm_bytes_per_launch")
+                    if pk.get("valu_frac") is not None:
+                        # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES of the profiled run (per-wave share of
+                        # cycles issuing VALU; BASELINE.md's VALU fraction beside the HBM fraction)
+                        k["valu_frac"] = pk["valu_frac"]
+                        k["wait_frac"] = pk.get("wait_frac")
                 ks[name] = k
             roof["kernels"] = ks
             roof["kernels_source"] = ("single-pipeline pass after the timed region (%d steps, every launch "
@@ -782,6 +809,9 @@ def main():
             dom = max(kernels, key=lambda q: kernels[q][0])
             roof["dominant_kernel"] = dom
             roof["dominant_ms_per_step"] = round(kernels[dom][0], 3)
+            if "valu_frac" in ks.get(dom, {}):
+                roof["valu_frac"] = ks[dom]["valu_frac"]
+                roof["valu_frac_source"] = "profiles/pmc_%s.json (dominant kernel, SQ counters)" % tag
         achieved = chain_gbps
         host = host_path(eng, echo, cfar, args) if (args.host_path and world == 1 and not win) else None
         # rank 0 only (the other ranks wait at the closing barrier); window mode: the reference

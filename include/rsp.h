@@ -179,9 +179,10 @@ const char* rsp_last_error(const rsp_ctx* ctx);
  * look-ahead frame); the default there is at least 16 pairs. */
 int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 
-/* Number of chunk pipelines (1..4; 0 = the default: 2, window mode 1): chunk k runs on the caller's stream or on
- * one of n-1 context-owned streams that fork from and join back into it, so consecutive
- * chunks overlap.  Each pipeline owns one PC scratch slot. */
+/* Number of chunk pipelines (1..4; 0 = the default: 2, window mode 1): chunk k runs on the
+ * caller's stream or on one of n-1 context-owned streams that fork from and join back into
+ * it, so consecutive chunks overlap.  Each pipeline owns one PC scratch slot (n = 1: every
+ * launch alone, for per-kernel timing). */
 int rsp_set_streams(rsp_ctx* ctx, int32_t n);
 
 /* ---- host-buffer entry points (MEX / fun_MTD_produce drop-in), synchronous ---------- */

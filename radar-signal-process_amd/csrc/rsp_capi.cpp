@@ -918,7 +918,10 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         }
     }
     if (cu > units) cu = units;
-    const int64_t nchunks = (units + cu - 1) / cu;
+    // Chunk boundaries: chunk k covers units [cstart[k], cstart[k + 1]), cu units each but the last.
+    std::vector<int64_t> cstart{0};
+    while (cstart.back() < units) cstart.push_back(cstart.back() + cu < units ? cstart.back() + cu : units);
+    const int64_t nchunks = (int64_t)cstart.size() - 1;
     const int ns = (int)(nsd < nchunks ? nsd : nchunks);
     const size_t plane = (size_t)V * Ro;                  // output cells per CPI
     const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
@@ -970,8 +973,8 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         const uint32_t* counts = nullptr;
     } pend[4];
     for (int64_t k = 0; k < nchunks; ++k) {
-        const int64_t u0 = k * cu;
-        const int64_t n = units - u0 < cu ? units - u0 : cu;
+        const int64_t u0 = cstart[(size_t)k];
+        const int64_t n = cstart[(size_t)k + 1] - u0;
         const int64_t ncpi = n * ocpi;                     // CPIs this chunk produces
         const size_t o0 = (size_t)u0 * ocpi * plane;      // output offset
         const int lane = (int)(k % ns);

@@ -27,6 +27,28 @@
 
 namespace rsp {
 
+#ifdef RSP_DIAG_STAMPS
+// Dev-only diagnostic build (tools/build_variant.sh, read by tools/diag_stamps.py): per-workgroup
+// phase timestamps of the PC and MTD kernels.  Lane 0 of wave 0 writes the shader clock
+// (s_memtime) at a phase boundary into an array no other code reads; a boundary marked `wait`
+// first waits for the wave's own memory operations, so "loads arrived" / "stores done" are
+// points in time.  Slots 8 and 9 hold the 100 MHz real-time clock at entry and exit; 10-12
+// split the FIR (staged, computed, stored).
+constexpr int kDiagSlots = 16, kDiagWG = 1 << 15;
+__device__ uint64_t g_diag[2][kDiagWG * kDiagSlots];
+__device__ __forceinline__ void diag_stamp(int k, int slot, bool wait, bool realtime = false) {
+    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t t = realtime ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+    const uint32_t wg = blockIdx.x + blockIdx.y * gridDim.x;
+    if (threadIdx.x == 0 && wg < (uint32_t)kDiagWG) g_diag[k][wg * kDiagSlots + slot] = t;
+}
+#define RSP_STAMP(k, slot, wait) diag_stamp(k, slot, wait)
+#define RSP_STAMP_RT(k, slot) diag_stamp(k, slot, false, true)
+#else
+#define RSP_STAMP(k, slot, wait) ((void)0)
+#define RSP_STAMP_RT(k, slot) ((void)0)
+#endif
+
 __device__ __forceinline__ float2 ld_c(const float2* p) { return *p; }
 __device__ __forceinline__ float2 ld_c(const __half2* p) { return __half22float2(*p); }
 __device__ __forceinline__ float2 ld_c(const double2* p) {
@@ -173,28 +195,45 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
+// The FIR segment's staging loads of a wave-uniform row (G % 64 == 0): the first B*G staged
+// samples (zeros before the segment and past in_len come from the buffer range check), issued
+// with the row's matched-filter loads so the two share one memory round trip.
+constexpr int kFirB = 8;
+template <typename TIn, int G>
+__device__ __forceinline__ void fir_stage_issue(float2 (&v)[kFirB], const TIn* __restrict__ x, const SegDev& g,
+                                                bool valid, int t, int i0) {
+    constexpr uint32_t ES = sizeof(TIn);
+    const int kp = g.ntaps4 - 1;
+    const auto xr = buf_rsrc(x + g.in_start, valid ? (uint32_t)g.in_len * ES : 0u);
+#pragma unroll
+    for (int q = 0; q < kFirB; ++q) {
+        const int j = i0 + q * G - kp;
+        v[q] = buf_ld_c((const TIn*)nullptr, xr, j >= 0 ? (uint32_t)j * ES : kOob, 0u);
+    }
+}
+
 template <typename TIn, int G, int SA = 0, bool WS = false>
 __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __restrict__ y,
                                         const SegDev& g, float* stage, bool valid, int t,
-                                        const float* __restrict__ gain, bool st_ok = true) {
+                                        const float* __restrict__ gain, bool st_ok = true,
+                                        const float2* pre = nullptr) {
     float2* s2 = reinterpret_cast<float2*>(stage);
     const int kp = g.ntaps4 - 1;
     const int len = g.out_len;
     const int nst = kp + len + 4;
     if constexpr (G % 64 == 0) {
         // The row is wave-uniform: stage through a range-checked buffer resource, 8 loads per
-        // thread issued together (zeros before the segment and past in_len come from the range
-        // check), so the staging costs one memory round trip instead of one per element step.
-        constexpr uint32_t ES = sizeof(TIn);
-        const auto xr = buf_rsrc(x + g.in_start, valid ? (uint32_t)g.in_len * ES : 0u);
+        // thread issued together, so the staging costs one memory round trip instead of one
+        // per element step; `pre` holds the first block's loads when the caller issued them.
         const auto gr = buf_rsrc(gain ? gain + g.in_start : nullptr, gain ? (uint32_t)g.in_len * 4u : 0u);
-        constexpr int B = 8;
+        constexpr int B = kFirB;
         for (int i0 = t; i0 < nst; i0 += B * G) {
             float2 v[B];
+            if (pre && i0 == t) {
 #pragma unroll
-            for (int q = 0; q < B; ++q) {
-                const int j = i0 + q * G - kp;
-                v[q] = buf_ld_c((const TIn*)nullptr, xr, j >= 0 ? (uint32_t)j * ES : kOob, 0u);
+                for (int q = 0; q < B; ++q) v[q] = pre[q];
+            } else {
+                fir_stage_issue<TIn, G>(v, x, g, valid, t, i0);
             }
             if (gain) {   // fused iSTC (wave-uniform)
 #pragma unroll
@@ -216,6 +255,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
         }
     }
     xsync<WS>();
+    RSP_STAMP(0, 10, false);
     const float2* __restrict__ taps = g.taps2_dev;
     for (int m0 = 4 * t; m0 < len; m0 += 4 * G) {
         float2 acc[4] = {};
@@ -225,7 +265,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
         w[4] = p[1];
         w[5] = p[2];
         w[6] = p[3];
-        for (int k = 0; k < g.ntaps4; k += 4) {
+        auto group = [&](int k) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) w[q] = p[q - 3 - k];
 #pragma unroll
@@ -237,7 +277,9 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             w[6] = w[2];
             w[5] = w[1];
             w[4] = w[0];
-        }
+        };
+        for (int k = 0; k < g.ntaps4; k += 4) group(k);
+        RSP_STAMP(0, 11, false);
         if (valid && st_ok) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -250,6 +292,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
             }
         }
     }
+    RSP_STAMP(0, 12, false);
     xsync<WS>();
 }
 
@@ -331,15 +374,25 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #pragma unroll
         for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
     }
+    // the FIR segment's staging loads ride on the same memory round trip (a second, dependent
+    // round trip made the short rows' FIR phase ~40 % of their lifetime: tools/diag_stamps.py)
+    float2 fpre[kUniform ? kFirB : 1];
+    if constexpr (kUniform) {
+        if (a.do_fir) fir_stage_issue<TIn, G>(fpre, x, a.fir, valid, t, t);
+    }
+    RSP_STAMP(0, 1, true);
     if (a.do_fir) {
         if (valid)
             for (int z = 0; z < a.nzero; ++z)
                 for (int c = a.zero_lo[z] + t; c < a.zero_hi[z]; c += G) st_c<SA>(y + c, make_float2(0.f, 0.f));
-        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t, a.gain, st_ok);
+        fir_row<TIn, G, SA, WS>(x, y, a.fir, reinterpret_cast<float*>(buf), valid, t, a.gain, st_ok,
+                                kUniform ? fpre : nullptr);
     }
+    RSP_STAMP(0, 2, false);
 #ifndef RSP_DIAG_PC_NOFFT   // dev-only diagnostic build: load, spectrum multiply, store (no FFTs)
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
 #endif
+    RSP_STAMP(0, 3, false);
     if constexpr (kEarly) {
 #pragma unroll
         for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hs[m]);   // conj(X.*H), 1/N in H
@@ -354,9 +407,11 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
         }
     }
+    RSP_STAMP(0, 4, false);
 #ifndef RSP_DIAG_PC_NOFFT
     fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
 #endif
+    RSP_STAMP(0, 5, false);
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, st_ok ? (uint32_t)out_len * 8u : 0u);
 #pragma unroll
@@ -368,6 +423,9 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             if (i < out_len) st_c<SA>(y + out_start + i, cconj(u[m]));
         }
     }
+    RSP_STAMP(0, 6, false);
+    RSP_STAMP(0, 7, true);
+    RSP_STAMP_RT(0, 9);
 }
 
 // Workgroup size shared by a pair of segment lengths: both run T threads (RPB = T/G rows).
@@ -383,32 +441,42 @@ struct PairCfg {
 
 // Single segment (N2 == 0) or two independent segments in one launch: blocks
 // [0, nblk2) run segment 2 (the long one, first for a short tail), the rest segment 1.
+// `bid` is the block's index among the PC blocks of the launch.
 template <typename TIn, int N1, int N2>
-#ifndef RSP_DIAG_PC_WAVES   // dev-only diagnostic build: minimum waves per SIMD of the PC kernel
-#define RSP_DIAG_PC_WAVES 2
-#endif
-__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_DIAG_PC_WAVES) void pc_mf_kernel(
-    const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
+__device__ __forceinline__ void pc_mf_block(const TIn* __restrict__ echo, float2* __restrict__ out, const PcMfArgs& a1,
+                                            const PcMfArgs& a2, int nblk2, int bid, float2* lds) {
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
     // unit u of a segment = (row u / nsub, overlap-save sub-block u % nsub)
     if constexpr (N2 != 0) {
-        if ((int)blockIdx.x < nblk2) {
+        if (bid < nblk2) {
             constexpr int G = PcCfg<N2>::G;
             const int grp = threadIdx.x / G, t = threadIdx.x % G;
-            const int u = blockIdx.x * PC::RPB2 + grp, ns = a2.nsub > 1 ? a2.nsub : 1;
+            const int ns = a2.nsub > 1 ? a2.nsub : 1;
+            const int u = bid * PC::RPB2 + grp;
             pc_row<TIn, N2, G, 0, G == 64>(echo, out, a2, u / ns, t, lds + grp * PcCfg<N2>::SLOT, u % ns);
             return;
         }
     }
     constexpr int G = PcCfg<N1>::G;
     const int grp = threadIdx.x / G, t = threadIdx.x % G;
-    const int b = (int)blockIdx.x - (N2 ? nblk2 : 0);
+    const int b = bid - (N2 ? nblk2 : 0);
     const int u = b * PC::RPB1 + grp, ns = a1.nsub > 1 ? a1.nsub : 1;   // (no FIR when ns > 1)
     // a row of one wave (G == 64) synchronises its exchanges within the wave: the rows of a
     // workgroup run independently instead of in barrier lockstep
     pc_row<TIn, N1, G, 0, G == 64>(echo, out, a1, u / ns, t, lds + grp * PcCfg<N1>::SLOT, u % ns);
+}
+
+#ifndef RSP_DIAG_PC_WAVES   // dev-only diagnostic build: minimum waves per SIMD of the PC kernel
+#define RSP_DIAG_PC_WAVES 2
+#endif
+template <typename TIn, int N1, int N2>
+__global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_DIAG_PC_WAVES) void pc_mf_kernel(
+    const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    RSP_STAMP(0, 0, false);
+    RSP_STAMP_RT(0, 8);
+    pc_mf_block<TIn, N1, N2>(echo, out, a1, a2, nblk2, (int)blockIdx.x, lds);
 }
 
 
@@ -483,6 +551,19 @@ static hipError_t launch_pc_mf_t(const TIn* echo, float2* out, const PcMfArgs& a
     }
 }
 #undef RSP_PAIR
+
+#ifdef RSP_DIAG_STAMPS
+}  // namespace rsp
+// Dev-only diagnostic export (not in include/rsp.h): copy kernel k's stamps (0 = PC, 1 = MTD)
+// of the last launch, kDiagSlots per workgroup, to host.
+extern "C" int rsp_diag_stamps(int k, uint64_t* host, int64_t n) {
+    if (k < 0 || k > 1 || n < 0 || n > (int64_t)rsp::kDiagWG * rsp::kDiagSlots) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsp::g_diag), (size_t)n * 8, (size_t)k * rsp::kDiagWG * rsp::kDiagSlots * 8,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+namespace rsp {
+#endif
 
 bool pc_pair_supported(int n1, int n2) {
     return (n1 == 1024 && (n2 == 1024 || n2 == 4096 || n2 == 8192 || n2 == 16384)) || (n1 == 512 && n2 == 1024);
@@ -949,7 +1030,9 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             }
         }
         if (b == 0) after_loads();
+        RSP_STAMP(1, 1, true);
         fft_reg_w<P, G, 1, E, 0, NW>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, tw);
+        RSP_STAMP(1, 2, false);
         if constexpr (BEAMS == 2) {
             if (b == 0) {
 #pragma unroll
@@ -999,6 +1082,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         if constexpr (SA != 0) buf_st_fa<SA>(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
         else buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
+    RSP_STAMP(1, 3, false);
     if (!a.cv.enabled) return;
     __syncthreads();  // the FFT exchange slots are free from here on
     float* mag = REF > 0 ? reinterpret_cast<float*>(smem) + c * C::MS2 + C::SPAD
@@ -1035,6 +1119,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         __syncthreads();
         doppler_flags<E>(mag, sums, a.cv, col_on, v0, v0 + E, o);
     }
+    RSP_STAMP(1, 4, false);
     if (o.fused && o.rflag) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1054,19 +1139,19 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 // P is the Doppler FFT length; a CPI supplies a.pin <= P pulses per beam (rows past pin are
 // the zero padding of fft(x, P, 1): out of the buffer's range, they load as 0).  BEAMS == 2:
 // the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
+// One MTD workgroup: tile bx (of gx along range) of launch CPI by (of gy); smem / s_hits: the
+// workgroup's dynamic LDS and hit counter.
 template <int P, int REF, int BEAMS>
-__global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) void mtd_kernel(const float2* __restrict__ pc,
-                                                     float* __restrict__ rdm,
-                                                     uint8_t* __restrict__ flagV, MtdArgs a) {
+__device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* __restrict__ rdm,
+                                          uint8_t* __restrict__ flagV, const MtdArgs& a, int bx, int by, int gx, int gy,
+                                          unsigned char* smem, uint32_t* s_hits) {
     using C = MtdCfg<P, BEAMS>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t s_hits;
-    const size_t cpi = blockIdx.y;
+    const size_t cpi = (size_t)by;
     const size_t R = (size_t)a.R_out;
     const size_t plane = (size_t)P * R;
     size_t row0 = cpi * (size_t)a.pin * BEAMS;                   // first PC row of this CPI
     if (a.nwin > 0) row0 = (cpi / a.nwin) * (size_t)a.pin + a.win_start[cpi % a.nwin];
-    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t wg = (uint32_t)by * (uint32_t)gx + (uint32_t)bx;
     MtdTile T;
     T.pc = pc + row0 * R;
     T.rdm = rdm + cpi * plane;
@@ -1076,27 +1161,43 @@ __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) voi
     T.hits = a.hits ? a.hits + (size_t)wg * (C::W * P) : nullptr;
     T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
     T.cell_base = (uint32_t)(cpi * plane);
-    T.bx = blockIdx.x;
+    T.bx = bx;
     if constexpr (C::W < 32) {   // 4 consecutive tiles on one XCD (workgroup x goes to XCD x % 8):
         // their partial RDM / flag lines (W = 16: 64-B RDM and 16-B flag row segments at c5)
         // meet in one L2 and leave it merged (c5 +1.5-2 %; at W = 32 the RDM segments are whole
         // 128-B lines and the grouping cost c3's MTD 3 %)
         constexpr int K = 4;
-        const int x = (int)blockIdx.x;
-        if (gridDim.x % (8 * K) == 0) T.bx = (x / (8 * K)) * (8 * K) + (x % 8) * K + (x / 8) % K;
+        const int x = bx;
+        if (gx % (8 * K) == 0) T.bx = (x / (8 * K)) * (8 * K) + (x % 8) * K + (x / 8) % K;
     }
-    const int nwg = (int)(gridDim.x * gridDim.y);
+    const int nwg = gx * gy;
     // one instance of the tile (the kernel's code stays ~half the size: it shares the
     // instruction cache with the PC kernel of the other pipeline); the range job is runtime-
     // guarded -- with n == 0 its hook and finish() return at once
     const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions &&
                      (uint64_t)a.prev_nregions * (uint64_t)a.prev_region < (uint64_t)(kOob / 4u);
     RangeJob57 rj;
+    RSP_STAMP(1, 0, false);
+    RSP_STAMP_RT(1, 8);
     if (job) rj.fetch_idx(a, (int)wg);
-    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, &s_hits, [&] { rj.fetch_cells(a); });
+    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, [&] { rj.fetch_cells(a); });
+    RSP_STAMP(1, 5, false);
     rj.finish(a);
+    RSP_STAMP(1, 6, false);
     if (job ? (rj.n > blockDim.x || a.prev_nregions > nwg) : a.prev_nregions > 0)
         prev_chunk_hits(a, (int)wg, nwg, job ? (int)blockDim.x : 0);
+    RSP_STAMP(1, 7, true);
+    RSP_STAMP_RT(1, 9);
+}
+
+template <int P, int REF, int BEAMS>
+__global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) void mtd_kernel(const float2* __restrict__ pc,
+                                                     float* __restrict__ rdm,
+                                                     uint8_t* __restrict__ flagV, MtdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_hits;
+    mtd_block<P, REF, BEAMS>(pc, rdm, flagV, a, (int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y, smem,
+                             &s_hits);
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
