@@ -20,6 +20,7 @@ tail -1 "$OUT/bench.log" | python -c "import json,sys; d=json.loads(sys.stdin.re
     || { echo "rocprof rc=$?"; tail -3 "$OUT/prof.log"; exit 1; }
 python tools/trace_summary.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/trace.json" > /dev/null
 python -c "import json; d=json.load(open('$OUT/trace.json')); print('trace span ms/step', d['span_ms_per_step'], {k: v['avg_us'] for k, v in d['kernels'].items()})"
+python tools/lane_overlap.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/overlap.json" > /dev/null || true
 # the same on ONE pipeline (--streams 1): kernels do not overlap, so rocprof's per-kernel averages
 # are comparable with bench.py's single-pipeline per-kernel entries
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof1" -o run -- \

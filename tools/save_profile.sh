@@ -8,6 +8,7 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 dst="$ROOT/profiles/$1/$2"; src="$ROOT/gpurun_out/$2"
 mkdir -p "$dst"
 cp "$src/bench.log" "$src/trace.json" "$src/pmc.json" "$src/pmc.txt" "$dst/"
+[ -f "$src/overlap.json" ] && cp "$src/overlap.json" "$dst/"
 cp "$src/prof/run_kernel_stats.csv" "$dst/kernel_stats.csv"
 if [ -f "$src/prof1/run_kernel_stats.csv" ]; then
   cp "$src/prof1/run_kernel_stats.csv" "$dst/kernel_stats_1pipeline.csv"; cp "$src/trace_1lane.json" "$dst/"
