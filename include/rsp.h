@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define RSP_ABI_VERSION 1
+#define RSP_ABI_VERSION 2   /* 2: rsp_set_fused / rsp_chain_check removed, rsp_set_pc_split added */
 #define RSP_MAX_SEG 4
 #define RSP_MAX_FIR_TAPS 64
 

@@ -254,7 +254,7 @@ static void zero_v_band(int64_t rows, int div, int* lo, int* hi) {
 }
 
 // ------------------------------------------------------------------ public API
-const char* rsp_version(void) { return "rsp-mi355x 0.1.0 (gfx950, abi 1)"; }
+const char* rsp_version(void) { return "rsp-mi355x 0.3.0 (gfx950, abi 2)"; }
 
 const char* rsp_last_error(const rsp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 

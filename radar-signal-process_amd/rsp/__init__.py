@@ -9,4 +9,4 @@ from . import _capi, presets, synth  # noqa: F401
 from ._capi import RspError, load_library  # noqa: F401
 from .engine import Engine, engine_for  # noqa: F401
 
-__version__ = "0.1.0"
+__version__ = "0.3.0"
