@@ -217,7 +217,7 @@ def pmc_traffic(tag):
 
 
 def bench_ingest(args, world, rank, local, dev, dist):
-    """--config ingest: frames/s through rsp_ingest_ddc_dev (record parse + DBF), v2 capture
+    """--config ingest: frames/s through rsp_ingest_frame_dev (record parse + DBF), v2 capture
     frames (332 PRTs x 3404 samples x 16 channels int16 I/Q -> 13 beams complex64), records
     resident in HBM; each rank decodes its own frames (no collective)."""
     import torch
@@ -288,7 +288,7 @@ def bench_ingest(args, world, rank, local, dev, dist):
             "config": {"workload": "ingest: %d frames per GPU per step, records resident in HBM" % B,
                        "prt": args.P, "samples": args.R, "channels": 16, "beams": 13,
                        "parallelism": "frame-sharded x%d, no collective" % world},
-            "roofline": {"bound": "hbm", "kernel": "ingest_ddc_kernel", "achieved": round(ach, 1),
+            "roofline": {"bound": "hbm", "kernel": "ingest_decode_kernel", "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
                          "traffic": None, "alg_bytes_per_unit": unit_bytes,
                          "avg_launch_us": round(per_frame_s * 1e6, 2),

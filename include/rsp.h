@@ -254,18 +254,27 @@ int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable);
  * (FrameDataRead_xzr.m:20-204, called at bin_to_mat_xzr.m:62).  The host reads the frame's
  * bytes from the cross-file stream (read_continuous_file_stream.m; rsp/ingest.py mirrors it)
  * and this call parses and beamforms them on the GPU.  Record = head (bytes_head, uint32
- * fields), realtime block, DDC payload int16 I/Q [sample][channel][I,Q] padded to 64 B, tail;
- * every PRT of a frame has the same record size (rsp_ingest_record_bytes).
- * Output: d_out[b * beam_stride + prt * point_prt + s] = sum_c (I + jQ)[s][c] * dbf[b][c]
+ * fields), realtime block, payload padded to 64 B (DDC: int16 I/Q [sample][channel][I,Q]),
+ * tail; in rsp_ingest_ddc_dev every PRT has the DDC record size (rsp_ingest_record_bytes).
+ * Output (DDC): d_out[b * beam_stride + prt * point_prt + s] = sum_c (I + jQ)[s][c] * dbf[b][c]
  * (sig_data_C * DBF_coeffs_data_C.', :158) as complex64, beam-major so each beam is the
  * [prt][sample] echo the chain reads; beam_stride = 0 means prt_num * point_prt (pass a larger
  * stride to land frames in a [beam][frames+1][P][R] window buffer).
  * d_status: int32[prt_num + 1], per-PRT RSP_PRT_* codes, and [prt_num] = rows decoded: the
  * frame stops at the first PRT the reference would return at (those rows and all later ones
  * are written as zeros, servo 0), so frameCompleted == (status[prt_num] == prt_num && no
- * RSP_PRT_TAIL_TRUNCATED).  Only DDC payloads (data_type 1) are built: ADC (type 0) cannot
- * pass the reference's own size check with beam_num != channel_num, and its 24-bit DBF branch
- * (type 2, :130-135) is marked unfinished there (uint8 arithmetic saturates). */
+ * RSP_PRT_TAIL_TRUNCATED).  rsp_ingest_ddc_dev decodes DDC payloads (data_type 1) only, every
+ * record sized by the params; rsp_ingest_frame_dev decodes every data type the reference
+ * parses, each record sized by its own head (:104-119), so a frame may mix types:
+ *   ADC (0): the int16 (samples x channels) matrix itself (:144-147) -- passes the size check
+ *            only with channel_num (of the head) == beam_num; beam b = (x_b, 0);
+ *   DBF (any other type): the 24-bit branch (:130-135,162-164) as MATLAB evaluates it -- its
+ *            data_temp is uint8, so b0 + b1*2^8 + b2*2^16 saturates to 255 once b1 or b2 is
+ *            non-zero (else b0) and the sign fix never fires; beam b = (v_2b, v_2b+1).  The
+ *            sizes pass only when the value count (2*ch for ch % 4 == 1, 2*ch + 2 for
+ *            ch % 4 == 0) is 2*beam_num; other channel counts are a MATLAB size error there and
+ *            RSP_PRT_BAD_SHAPE here.  (The reference marks this branch unfinished.)
+ * The two calls share per-context scratch: one frame at a time per context. */
 typedef struct {
     int32_t prt_num;         /* Sig_Config.prtNum (332) */
     int32_t point_prt;       /* Sig_Config.point_PRT (3404) */
@@ -282,7 +291,7 @@ enum {
     RSP_PRT_TAIL_TRUNCATED = 2,   /* decoded, but the tail is cut: the frame ends incomplete */
     RSP_PRT_BAD_COUNT = 3,        /* pulse_data_num <= 0 (FrameDataRead_xzr.m:90-94) */
     RSP_PRT_BAD_SHAPE = 4,        /* pulse_data_num != point_prt or channels != channel_num */
-    RSP_PRT_UNSUPPORTED_TYPE = 5  /* data_type != 1 (DDC) */
+    RSP_PRT_UNSUPPORTED_TYPE = 5  /* data_type != 1 (DDC) in rsp_ingest_ddc_dev */
 };
 
 /* Bytes of one DDC PRT record of this shape. */
@@ -292,6 +301,11 @@ int rsp_ingest_record_bytes(const rsp_ingest_params* p, int64_t* bytes);
 int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
                        const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
                        int32_t* d_status, void* stream);
+/* Every data type, records sized by their heads (the same arguments; d_dbf is read by DDC
+ * records only). */
+int rsp_ingest_frame_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
+                         const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
+                         int32_t* d_status, void* stream);
 
 /* ---- post-detection measurement --------------------------------------- */
 /* Range / velocity / elevation of every CFAR hit, replacing

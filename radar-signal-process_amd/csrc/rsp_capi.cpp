@@ -59,6 +59,7 @@ struct rsp_ctx {
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
     DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
+    DevBuf ing_meta;                    // ingest: per-PRT record offsets and types
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
     // diagnostics (rsp_profile): HIP event pairs around each kernel launch
     struct Ev {
@@ -264,7 +265,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
-                      &ctx->meas_band};
+                      &ctx->meas_band, &ctx->ing_meta};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -1240,22 +1241,29 @@ int rsp_ingest_record_bytes(const rsp_ingest_params* p, int64_t* bytes) {
     return ingest_shape(nullptr, p, bytes);
 }
 
-int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
-                       const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
-                       int32_t* d_status, void* stream) {
-    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_ingest_ddc_dev: null ctx");
+static int ingest_run(rsp_ctx* ctx, const char* who, bool ddc_only, const uint8_t* d_stream, int64_t nbytes,
+                      const rsp_ingest_params* p, const float* d_dbf, void* d_out, int64_t beam_stride,
+                      uint16_t* d_servo, int32_t* d_status, void* stream) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "%s: null ctx", who);
     int64_t rec = 0;
     int rc = ingest_shape(ctx, p, &rec);
     if (rc) return rc;
     if (!d_stream || nbytes < 0 || !d_dbf || !d_out || !d_status)
-        return fail(ctx, RSP_ERR_ARG, "rsp_ingest_ddc_dev: null buffer or negative byte count");
+        return fail(ctx, RSP_ERR_ARG, "%s: null buffer or negative byte count", who);
     const int64_t plane = (int64_t)p->prt_num * p->point_prt;
     if (beam_stride == 0) beam_stride = plane;
-    if (beam_stride < plane) return fail(ctx, RSP_ERR_ARG, "rsp_ingest_ddc_dev: beam_stride %lld < prt*point %lld",
+    if (beam_stride < plane) return fail(ctx, RSP_ERR_ARG, "%s: beam_stride %lld < prt*point %lld", who,
                                          (long long)beam_stride, (long long)plane);
     if (p->prt_num == 0) return RSP_OK;
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    // per-PRT record offsets and types, written by the check kernel for the decode kernel
+    // (stream-ordered on the caller's stream; one frame at a time per context)
+    rc = ensure(ctx, ctx->ing_meta, (size_t)p->prt_num * (sizeof(int64_t) + sizeof(int32_t)));
+    if (rc) return rc;
     rsp::IngestArgs a{};
+    a.ddc_only = ddc_only ? 1 : 0;
+    a.offs = (int64_t*)ctx->ing_meta.p;
+    a.types = (int32_t*)((int64_t*)ctx->ing_meta.p + p->prt_num);
     a.prt_num = p->prt_num;
     a.point_prt = p->point_prt;
     a.channel_num = p->channel_num;
@@ -1265,9 +1273,23 @@ int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, co
     a.bytes_tail = p->bytes_tail;
     a.rec_bytes = rec;
     a.beam_stride = beam_stride;
-    HIP_TRY(ctx, rsp::launch_ingest_ddc(d_stream, nbytes, a, (const float2*)d_dbf, (float2*)d_out, d_servo, d_status,
-                                        (hipStream_t)stream));
+    HIP_TRY(ctx, rsp::launch_ingest(d_stream, nbytes, a, (const float2*)d_dbf, (float2*)d_out, d_servo, d_status,
+                                    (hipStream_t)stream));
     return RSP_OK;
+}
+
+int rsp_ingest_ddc_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
+                       const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
+                       int32_t* d_status, void* stream) {
+    return ingest_run(ctx, "rsp_ingest_ddc_dev", true, d_stream, nbytes, p, d_dbf, d_out, beam_stride, d_servo,
+                      d_status, stream);
+}
+
+int rsp_ingest_frame_dev(rsp_ctx* ctx, const uint8_t* d_stream, int64_t nbytes, const rsp_ingest_params* p,
+                         const float* d_dbf, void* d_out, int64_t beam_stride, uint16_t* d_servo,
+                         int32_t* d_status, void* stream) {
+    return ingest_run(ctx, "rsp_ingest_frame_dev", false, d_stream, nbytes, p, d_dbf, d_out, beam_stride, d_servo,
+                      d_status, stream);
 }
 
 // ------------------------------------------------------------------ host-buffer entry points

@@ -168,11 +168,33 @@ hipError_t launch_prefilter(const float2* in, float2* out, const float* gain, in
 struct IngestArgs {
     int prt_num, point_prt, channel_num, beam_num;
     int bytes_head, bytes_realtime, bytes_tail;
-    int64_t rec_bytes;       // head + realtime + payload (padded to 64 B) + tail
+    int64_t rec_bytes;       // head + realtime + payload (padded to 64 B) + tail of a DDC record
     int64_t beam_stride;     // output elements between consecutive beams' [prt][sample] planes
+    int ddc_only;            // rsp_ingest_ddc_dev: records sized by the params, other types refused
+    int64_t* offs;           // [prt_num] record offsets in the stream (check -> decode kernel)
+    int32_t* types;          // [prt_num] data types of the decoded records
 };
-hipError_t launch_ingest_ddc(const uint8_t* stream, int64_t nbytes, const IngestArgs& a, const float2* dbf,
-                             float2* out, uint16_t* servo, int32_t* status, hipStream_t s);
+hipError_t launch_ingest(const uint8_t* stream, int64_t nbytes, const IngestArgs& a, const float2* dbf,
+                         float2* out, uint16_t* servo, int32_t* status, hipStream_t s);
+
+// Payload bytes of one record by data type (FrameDataRead_xzr.m:104-119): ADC (0) int16 per
+// channel, DDC (1) int16 I/Q per channel, anything else the 24-bit DBF layout (3-byte I/Q per
+// channel plus 8 - mod(6*ch, 8) pad bytes per sample), the whole padded to 64 B.
+constexpr int64_t ingest_payload_bytes(uint32_t type, int64_t pdn, int64_t ch) {
+    const int64_t sig = type == 0 ? pdn * ch * 2
+                      : type == 1 ? pdn * ch * 4
+                                  : pdn * ch * 6 + pdn * (8 - (6 * ch) % 8);
+    return sig % 64 ? sig + 64 - sig % 64 : sig;
+}
+// 24-bit DBF branch (FrameDataRead_xzr.m:130-135,162-164): bytes per sample row, and the number
+// of values the three column ranges 1:3:end-3, 2:3:end-2, 3:3:end give (-1 when their lengths
+// differ or the count is odd: the reference's own sum or I/Q pairing raises a size error).
+constexpr int dbf24_row_bytes(int ch) { return 6 * ch + (8 - (6 * ch) % 8); }
+constexpr int dbf24_values(int ch) {
+    const int L = dbf24_row_bytes(ch);
+    const int n1 = L - 3 >= 1 ? (L - 4) / 3 + 1 : 0, n2 = L - 2 >= 2 ? (L - 4) / 3 + 1 : 0, n3 = L / 3;
+    return (n1 == n2 && n2 == n3 && n1 % 2 == 0) ? n1 : -1;
+}
 
 bool mtd_size_supported(int P, int beams = 1);
 bool pc_nfft_supported(int n);

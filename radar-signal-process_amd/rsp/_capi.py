@@ -30,7 +30,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_ingest_record_bytes",
-           "rsp_ingest_ddc_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter")
+           "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter")
 RSP_NKERNELS = 4
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
 
@@ -144,6 +144,8 @@ def load_library(path=None):
     lib.rsp_ingest_record_bytes.argtypes = [C.POINTER(rsp_ingest_params), C.POINTER(i64)]
     lib.rsp_ingest_ddc_dev.restype = C.c_int
     lib.rsp_ingest_ddc_dev.argtypes = [vp, vp, i64, C.POINTER(rsp_ingest_params), vp, vp, i64, vp, vp, vp]
+    lib.rsp_ingest_frame_dev.restype = C.c_int
+    lib.rsp_ingest_frame_dev.argtypes = [vp, vp, i64, C.POINTER(rsp_ingest_params), vp, vp, i64, vp, vp, vp]
     lib.rsp_motion_measure_dev.restype = C.c_int
     lib.rsp_motion_measure_dev.argtypes = [vp, vp, vp, vp, i64, i64, i64, C.POINTER(rsp_measure_params), vp, vp,
                                            i64, vp, vp, vp, vp]

@@ -8,16 +8,17 @@ Mirrors the reference's reader stack with the same names and argument meaning:
     advances it again, so that file's successor is skipped (quirk=False reads straight on)
   * FrameDataRead_xzr(stream, DBF_coeffs_data_C, Sig_Config, frameRInd)
         -> (sig_data_DBF_allprts, servo_angle, frameCompleted, is_global_stream_end)
-    FrameDataRead_xzr.m:20-204, with the parse and the DBF product on the GPU
-    (rsp_ingest_ddc_dev, csrc/rsp_ingest.hip).  sig_data_DBF_allprts is a torch complex64
-    tensor on the device in the chain's layout [beam][prt][sample] (MATLAB's is
-    prt x sample x beam: .permute(1, 2, 0)).
+    FrameDataRead_xzr.m:20-204, with the parse, the payload decode of every data type (DDC
+    + DBF product, ADC, the 24-bit DBF branch) on the GPU (rsp_ingest_frame_dev,
+    csrc/rsp_ingest.hip).  sig_data_DBF_allprts is a torch complex64 tensor on the device in
+    the chain's layout [beam][prt][sample] (MATLAB's is prt x sample x beam: .permute(1, 2, 0)).
   * read_dbf_coeffs(path)                                bin_to_mat_xzr.m:22-29
 
-The host reads each record as the reference does (head, realtime block, payload, tail, each
-one read through the stream, so file-boundary behaviour matches) into one buffer per frame;
-the record sizes come from Sig_Config (uniform DDC records), and the GPU checks every head
-against them.  No CPU fallback: the parse and the beamforming run only in librsp.so.
+The host reads each record as the reference does (head, realtime block, payload sized by the
+head, tail, each one read through the stream and stopping where the reference returns, so the
+stream position and file-boundary behaviour match) into one buffer per frame; the GPU then
+locates and checks every record itself.  No CPU fallback: the parse, the decode and the
+beamforming run only in librsp.so.
 """
 import ctypes as C
 import os
@@ -121,6 +122,37 @@ def read_dbf_coeffs(path):
     return m[:, 0::2] + 1j * m[:, 1::2]
 
 
+def payload_bytes(data_type, pdn, ch):
+    """FrameDataRead_xzr.m:105-119: a record's signal bytes by data type, padded to 64 B."""
+    if data_type == 0:
+        sig = pdn * ch * 2
+    elif data_type == 1:
+        sig = pdn * ch * 4
+    else:
+        sig = pdn * ch * 6 + pdn * (8 - (6 * ch) % 8)
+    return sig + (64 - sig % 64 if sig % 64 else 0)
+
+
+def dbf24_values(ch):
+    """Values per sample row of the 24-bit DBF branch (:132-133, three column ranges), or -1
+    where MATLAB raises a size error (unequal ranges or an odd count at :163)."""
+    L = 6 * ch + (8 - (6 * ch) % 8)
+    n1, n2, n3 = len(range(0, L - 3, 3)), len(range(1, L - 2, 3)), len(range(2, L, 3))
+    return n1 if n1 == n2 == n3 and n1 % 2 == 0 else -1
+
+
+def _shape_ok(data_type, pdn, ch, cfg):
+    """Whether the reference gets past :171-176 (and :158's inner dimension for DDC) -- the host
+    needs it only to stop reading where the reference does (before the tail)."""
+    if pdn != cfg["point_PRT"]:
+        return False
+    if data_type == 1:
+        return ch == cfg["channel_num"]
+    if data_type == 0:
+        return ch == cfg["beam_num"]
+    return dbf24_values(ch) == 2 * cfg["beam_num"]
+
+
 def sig_config(prtNum=332, point_PRT=3404, channel_num=16, beam_num=13, bytesFrameHead=64,  # noqa: N803
                bytesFrameEnd=64, bytesFrameRealtime=128, fs=100e6, timer_freq=200e6):
     """bin_to_mat_xzr.m:35-43 (field names as there)."""
@@ -172,8 +204,9 @@ class Ingest:
         d = np.ascontiguousarray(np.stack([np.real(dbf_C), np.imag(dbf_C)], axis=-1), dtype=np.float32)
         return torch.from_numpy(d).to(self.device)
 
-    def decode_dev(self, d_stream, nbytes, cfg, d_dbf, out=None, beam_stride=0, stream=None):
-        """rsp_ingest_ddc_dev on device buffers; returns (out, servo uint16, status int32)."""
+    def decode_dev(self, d_stream, nbytes, cfg, d_dbf, out=None, beam_stride=0, stream=None, ddc_only=False):
+        """rsp_ingest_frame_dev (every data type, records sized by their heads) or, ddc_only,
+        rsp_ingest_ddc_dev on device buffers; returns (out, servo uint16, status int32)."""
         import torch
         P, R, B = cfg["prtNum"], cfg["point_PRT"], cfg["beam_num"]
         if out is None:
@@ -181,24 +214,36 @@ class Ingest:
         servo = torch.empty((P,), dtype=torch.int16, device=self.device)
         status = torch.empty((P + 1,), dtype=torch.int32, device=self.device)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        capi.check(self.lib.rsp_ingest_ddc_dev(
+        fn = self.lib.rsp_ingest_ddc_dev if ddc_only else self.lib.rsp_ingest_frame_dev
+        capi.check(fn(
             self.ctx, C.c_void_p(d_stream.data_ptr()), int(nbytes), C.byref(self.params(cfg)),
             C.c_void_p(d_dbf.data_ptr()), C.c_void_p(out.data_ptr()), int(beam_stride),
             C.c_void_p(servo.data_ptr()), C.c_void_p(status.data_ptr()), C.c_void_p(s.cuda_stream)), self.ctx)
         return out, servo, status
 
-    def read_frame_bytes(self, stream, cfg):
-        """The frame's records as the reference reads them (head, realtime, payload, tail per
-        PRT); stops at the first short read.  Returns (bytes, stream_ended)."""
-        rec = self.record_bytes(cfg)
+    @staticmethod
+    def read_frame_bytes(stream, cfg):
+        """The frame's records as the reference reads them (FrameDataRead_xzr.m:57-189: head,
+        then -- unless pulse_data_num is 0 -- realtime block, payload sized by the head's type,
+        samples and channels, and -- unless the size check fails -- tail), stopping where it
+        returns.  Returns (bytes, stream_ended)."""
         bh, br, bt = cfg["bytesFrameHead"], cfg["bytesFrameRealtime"], cfg["bytesFrameEnd"]
         parts = []
+
+        def take(n):
+            data, got, end = stream.read(n)
+            parts.append(data)
+            return not (end or got < n)
+
         for _ in range(cfg["prtNum"]):
-            for n in (bh, br, rec - bh - br - bt, bt):
-                data, got, end = stream.read(n)
-                parts.append(data)
-                if end or got < n:
-                    return b"".join(parts), True
+            if not take(bh):
+                return b"".join(parts), True
+            head = np.frombuffer(parts[-1][:32], dtype="<u4")
+            pdn, ch, typ = int(head[6]), int(head[3] & 0xff), int(head[7] & 0xff)
+            if pdn == 0 or not take(br) or not take(payload_bytes(typ, pdn, ch)):
+                return b"".join(parts), True
+            if not _shape_ok(typ, pdn, ch, cfg) or not take(bt):
+                return b"".join(parts), True
         return b"".join(parts), False
 
     def FrameDataRead_xzr(self, stream, DBF_coeffs_data_C, Sig_Config, frameRInd):  # noqa: N802,N803

@@ -34,6 +34,38 @@ def synth_frame(prt, point, ch, beams, seed, frame_no=0):
     return iq, dbf, servo, cfg, stream
 
 
+def synth_mixed_frame(types, point, ch, beams, seed, channel_num=None):
+    """A frame whose PRT p carries data type types[p]: DDC (1) int16 I/Q, ADC (0) int16 per
+    channel, or the 24-bit DBF layout (2) -- random bytes where the middle and high byte of a
+    value are zero half the time each, so the uint8 arithmetic gives both saturated and plain
+    values.  Returns (dbf, cfg, stream)."""
+    rng = np.random.default_rng(seed)
+    prt = len(types)
+    cn = ch if channel_num is None else channel_num
+    ang = rng.uniform(-np.pi, np.pi, size=(beams, cn))
+    dbf = np.exp(1j * ang) * rng.uniform(0.5, 1.0, size=(beams, cn))
+    cfg = dict(prtNum=prt, point_PRT=point, channel_num=cn, beam_num=beams, bytesFrameHead=64,
+               bytesFrameEnd=64, bytesFrameRealtime=128)
+    recs = []
+    for p, t in enumerate(types):
+        shape = np.zeros((point, ch), dtype=np.int8)
+        if t == 1:
+            iq = rng.integers(-30000, 30000, size=(point, ch, 2), dtype=np.int16)
+            recs.append(ref.prt_record(iq, pulse_no=p, servo=p * 7, pulse_num=prt, cfg=cfg))
+            continue
+        if t == 0:
+            pay = rng.integers(-32768, 32768, size=(point, ch), dtype=np.int16).astype("<i2").tobytes()
+        else:
+            L = 6 * ch + (8 - (6 * ch) % 8)
+            b = rng.integers(0, 256, size=(point, L), dtype=np.uint8)
+            keep = rng.random(size=(point, L)) < 0.5
+            col = np.arange(L) % 3
+            b[(col > 0)[None, :] & ~keep] = 0
+            pay = b.tobytes()
+        recs.append(ref.prt_record(shape, pulse_no=p, servo=p * 7, pulse_num=prt, cfg=cfg, data_type=t, payload=pay))
+    return dbf, cfg, b"".join(recs)
+
+
 def main():
     prt, point, ch, beams = 6, 40, 16, 13
     iq, dbf, servo, cfg, stream = synth_frame(prt, point, ch, beams, seed=2001)

@@ -1,9 +1,10 @@
-"""GPU parity of the ingest path (rsp_ingest_ddc_dev through rsp.ingest) against the fp64
-oracle restatement of FrameDataRead_xzr.m (oracle/ingest_ref.py).
+"""GPU parity of the ingest path (rsp_ingest_frame_dev / rsp_ingest_ddc_dev through
+rsp.ingest) against the fp64 oracle restatement of FrameDataRead_xzr.m (oracle/ingest_ref.py).
 
-Bars: DBF beams rel-err <= 1e-6 (Frobenius, fp32 accumulation of int16 samples against
-fp64); servo angles, per-PRT stop position and the zero rows after it bit-exact; the frame
-flags (frameCompleted, is_global_stream_end) equal.
+Bars: DDC beams rel-err <= 1e-6 (Frobenius, fp32 accumulation of int16 samples against
+fp64); ADC and 24-bit DBF rows bit-exact (small integers); servo angles, per-PRT stop position
+and the zero rows after it bit-exact; the frame flags (frameCompleted, is_global_stream_end)
+equal.
 """
 import os
 import sys
@@ -14,7 +15,7 @@ import pytest
 import ingest_ref as ref
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
-from make_golden_ingest import synth_frame  # noqa: E402
+from make_golden_ingest import synth_frame, synth_mixed_frame  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-6
@@ -144,3 +145,70 @@ def test_files_and_window_placement(ing, tmp_path):
     for f, s in enumerate((s0, s1)):
         want, _, _, _ = ref.FrameReader().read(ref.BytesStream(s), dbf, cfg, 0)
         assert _rel(win[:, f].permute(1, 2, 0).cpu().numpy(), want) < TOL
+
+
+def _exact_rows(got, want, types):
+    for p, t in enumerate(types):
+        if t != 1:
+            np.testing.assert_array_equal(got[p], want[p])
+
+
+def test_adc_frame(ing):
+    """ADC records (FrameDataRead_xzr.m:144-147): with channel_num == beam_num the int16
+    matrix is the frame's beams, bit-exact."""
+    types = [0] * 6
+    dbf, cfg, stream = synth_mixed_frame(types, 3404, 13, 13, seed=21)
+    got, done = _check(ing, stream, dbf, cfg)
+    assert done
+    want, _, _, _ = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    _exact_rows(got, want, types)
+
+
+@pytest.mark.parametrize("ch,beams", [(16, 17), (13, 13), (4, 5)])
+def test_dbf24_frame(ing, ch, beams):
+    """The 24-bit DBF branch as MATLAB's uint8 arithmetic evaluates it, bit-exact."""
+    types = [2] * 5
+    dbf, cfg, stream = synth_mixed_frame(types, 1000, ch, beams, seed=ch)
+    got, done = _check(ing, stream, dbf, cfg)
+    assert done
+    want, _, _, _ = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    _exact_rows(got, want, types)
+
+
+def test_mixed_frame_and_cuts(ing):
+    """A frame of DDC, ADC and DBF records (9 channels and 9 beams pass all three size checks):
+    records are located by walking the heads from the first one whose size differs, and cuts
+    inside each kind of record stop the frame where the reference stops."""
+    types = [1, 1, 0, 2, 2, 1, 0, 1, 2, 1, 1, 1]
+    dbf, cfg, stream = synth_mixed_frame(types, 3404, 9, 9, seed=33)
+    got, done = _check(ing, stream, dbf, cfg)
+    assert done
+    want, _, _, _ = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    _exact_rows(got, want, types)
+    offs = [0]
+    for t in types:
+        offs.append(offs[-1] + 192 + ref.payload_bytes(t, 3404, 9) + 64)
+    for p in (2, 3, 6, 9):   # inside the payload, then inside the tail
+        _check(ing, stream[:offs[p] + 192 + 1000], dbf, cfg)
+        _check(ing, stream[:offs[p + 1] - 10], dbf, cfg)
+
+
+def test_dbf24_size_error_and_ddc_only(ing):
+    """14 channels give an odd 24-bit value count: a MATLAB size error in the reference,
+    RSP_PRT_BAD_SHAPE here; rsp_ingest_ddc_dev refuses the first non-DDC record."""
+    import torch
+    from rsp import _capi
+    dbf, cfg, stream = synth_mixed_frame([1, 2, 1], 100, 14, 7, seed=3)
+    with pytest.raises(ValueError):
+        ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    d = torch.frombuffer(bytearray(stream), dtype=torch.uint8).cuda()
+    out, _, status = ing.decode_dev(d, len(stream), cfg, ing.dbf_device(dbf))
+    st = status.cpu().numpy()
+    assert st[0] == _capi.RSP_PRT_OK and st[1] == _capi.RSP_PRT_BAD_SHAPE and st[3] == 1
+    assert not out[:, 1:].any().item() and out[:, 0].abs().sum().item() > 0
+    types = [1, 1, 0, 1]
+    dbf, cfg, stream = synth_mixed_frame(types, 100, 9, 9, seed=4)
+    d = torch.frombuffer(bytearray(stream), dtype=torch.uint8).cuda()
+    _, _, status = ing.decode_dev(d, len(stream), cfg, ing.dbf_device(dbf), ddc_only=True)
+    st = status.cpu().numpy()
+    assert st[2] == _capi.RSP_PRT_UNSUPPORTED_TYPE and st[4] == 2

@@ -11,7 +11,7 @@ import pytest
 import ingest_ref as ref
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
-from make_golden_ingest import synth_frame  # noqa: E402
+from make_golden_ingest import synth_frame, synth_mixed_frame  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ingest_6x40.npz")
 
@@ -120,3 +120,84 @@ def test_record_bytes_abi():
     assert n.value == 64 + 128 + ref.ddc_payload_bytes(37, 3) + 64 == 64 + 128 + 448 + 64
     bad = ingest.sig_config(point_PRT=0)
     assert lib.rsp_ingest_record_bytes(C.byref(ingest.Ingest.params(bad)), C.byref(n)) == _capi.RSP_ERR_ARG
+
+
+def _direct_dbf24(raw, pdn, ch, beams):
+    """The 24-bit branch's result written out directly: value j of a sample row is 255 when
+    its middle or high byte is non-zero (uint8 saturation), else its low byte."""
+    L = 6 * ch + (8 - (6 * ch) % 8)
+    rows = np.frombuffer(raw[:pdn * L], dtype=np.uint8).reshape(pdn, L).astype(np.int64)
+    v = np.where((rows[:, 1:3 * 2 * beams:3] | rows[:, 2:3 * 2 * beams:3]) != 0, 255, rows[:, 0:3 * 2 * beams:3])
+    return v[:, 0::2] + 1j * v[:, 1::2]
+
+
+@pytest.mark.parametrize("ch,beams", [(16, 17), (13, 13), (4, 5), (9, 9)])
+def test_oracle_dbf24_literal(ch, beams):
+    """FrameDataRead_xzr.m:130-135,162-164 with MATLAB's uint8 arithmetic: the oracle's
+    column ranges and saturating sums equal the direct formulation, and the value count the
+    product's size check uses (rsp.ingest.dbf24_values) is the oracle's column count."""
+    from rsp import ingest
+    dbf, cfg, stream = synth_mixed_frame([2, 2, 2], 23, ch, beams, seed=ch)
+    assert ingest.dbf24_values(ch) == 2 * beams
+    out, _, done, end = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    assert done and not end
+    rec = len(stream) // 3
+    for p in range(3):
+        raw = stream[p * rec + 64 + 128:(p + 1) * rec - 64]
+        np.testing.assert_array_equal(out[p], _direct_dbf24(raw, 23, ch, beams))
+    vals = np.concatenate([out.real.ravel(), out.imag.ravel()])
+    assert (vals == 255).any() and ((vals > 0) & (vals < 255)).any()
+
+
+@pytest.mark.parametrize("ch", [2, 3, 6, 7, 14])
+def test_oracle_dbf24_size_errors(ch):
+    """Channel counts whose 24-bit rows give unequal column ranges or an odd value count are a
+    MATLAB size error in the reference (the product reports RSP_PRT_BAD_SHAPE)."""
+    from rsp import ingest
+    assert ingest.dbf24_values(ch) == -1
+    dbf, cfg, stream = synth_mixed_frame([2], 10, ch, 4, seed=ch)
+    with pytest.raises(ValueError):
+        ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+
+
+def test_oracle_adc_and_mixed_frame():
+    """ADC records are the int16 matrix itself (:144-147) and records of different types and
+    sizes follow one another (each sized by its own head, :105-119)."""
+    types = [1, 0, 2, 2, 1, 0, 1]
+    dbf, cfg, stream = synth_mixed_frame(types, 31, 9, 9, seed=4)
+    out, ang, done, end = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    assert done and not end
+    off = 0
+    for p, t in enumerate(types):
+        size = ref.payload_bytes(t, 31, 9)
+        raw = stream[off + 192:off + 192 + size]
+        if t == 0:
+            np.testing.assert_array_equal(out[p], np.frombuffer(raw[:31 * 9 * 2], "<i2").reshape(31, 9))
+        elif t == 2:
+            np.testing.assert_array_equal(out[p], _direct_dbf24(raw, 31, 9, 9))
+        off += 192 + size + 64
+    assert off == len(stream)
+    np.testing.assert_array_equal(ang, 7 * np.arange(len(types)))
+
+
+def test_host_reader_stops_where_the_reference_does():
+    """rsp.ingest.Ingest.read_frame_bytes reads exactly the bytes the oracle's reader consumes
+    (a record sized by its head; no realtime block after pulse_data_num = 0; no tail after a
+    failed size check), so the stream position after a frame matches."""
+    from rsp import ingest
+    types = [1, 0, 2, 1]
+    dbf, cfg, stream = synth_mixed_frame(types, 20, 9, 9, seed=6)
+    rec0 = 64 + 128 + ref.payload_bytes(1, 20, 9) + 64
+    cases = {"full": stream, "cut": stream[:rec0 + 100]}
+    b = bytearray(stream)
+    b[rec0 + 12:rec0 + 16] = (5).to_bytes(4, "little")       # PRT 1 (ADC): 5 channels != 9 beams
+    cases["shape"] = bytes(b)
+    b = bytearray(stream)
+    b[rec0 + 24:rec0 + 28] = (0).to_bytes(4, "little")       # PRT 1: pulse_data_num = 0
+    cases["count"] = bytes(b)
+    for name, s in cases.items():
+        host, oracle = ingest.BytesStream(s), ref.BytesStream(s)
+        data, ended = ingest.Ingest.read_frame_bytes(host, cfg)
+        _, _, done, end = ref.FrameReader().read(oracle, dbf, cfg, 0)
+        assert host._pos == oracle.pos == len(data), name
+        assert ended == end, name
