@@ -30,6 +30,8 @@ HBM_PEAK_GBPS = 8000.0
 
 # BASELINE.json configs.  mode "window": batch = frame pairs per GPU per step,
 # each giving `win` windowed CPIs (MTD/main_produce_dataset_win_xzr_v2.m:94-144).
+WARMUP_S = 0.3   # default warmup: seconds of device work before the timed region
+
 CONFIGS = {
     "c2": dict(P=128, R=4096, batch=256, cfar=False, half=False, win=0),
     "c3": dict(P=128, R=4096, batch=1024, cfar=True, half=False, win=0),
@@ -48,7 +50,10 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3, help=">= 1 (the first warmup step counts launches)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warmup steps, >= 1 (the first one counts launches); default: as many as "
+                         "fill %.1f s of device work, at least 3 -- the GPU's clocks ramp up over its first "
+                         "~50 ms of work (tools/warmup_probe.py: c3 4.1 -> 3.55 ms per step)" % WARMUP_S)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--preset", default="v2", choices=["v2", "dmx"])
     ap.add_argument("--P", type=int, default=None)
@@ -239,8 +244,7 @@ def bench_ingest(args, world, rank, local, dev, dist):
         for f in range(B):
             ing.decode_dev(frames[f * nb:(f + 1) * nb], nb, cfg, d_dbf, out=out[f], stream=stream)
 
-    for _ in range(args.warmup):
-        step()
+    warm(step, args, dev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -304,8 +308,7 @@ def bench_ingest(args, world, rank, local, dev, dist):
 def _timed(args, world, dev, dist, stream, step):
     """W warmup steps, then K timed steps between barrier + synchronize; (wall s, event ms)."""
     import torch
-    for _ in range(args.warmup):
-        step()
+    warm(step, args, dev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -432,8 +435,7 @@ def bench_measure(args, world, rank, local, dev, dist):
                                              cells.data_ptr(), count.data_ptr(), C.c_void_p(stream.cuda_stream))
         assert rc == 0
 
-    for _ in range(args.warmup):
-        step()
+    warm(step, args, dev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -587,6 +589,22 @@ def rank_plan(args, rank):
     return {"rank": rank, "cpis": [lo, hi], "seed": 1000 + cfg_id + lo}
 
 
+def warm(step, args, dev):
+    """The untimed warmup: args.warmup steps, or (None) steps until WARMUP_S seconds of device
+    work have run (at least 3); args.warmup is set to the count used (the JSON reports it)."""
+    import torch
+    if args.warmup is not None:
+        for _ in range(args.warmup):
+            step()
+        return
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or time.perf_counter() - t0 < WARMUP_S:
+        step()
+        n += 1
+        torch.cuda.synchronize(dev)
+    args.warmup = n
+
+
 def dry_run(args, world, rank, dist):
     """--dry-run: the multi-rank path without a GPU -- gloo rendezvous, each rank's shard plan,
     a stub step (sleep), barrier + max-over-ranks timing, the per-rank step times and the JSON
@@ -599,6 +617,7 @@ def dry_run(args, world, rank, dist):
     def barrier():
         if world > 1:
             dist.barrier()
+    args.warmup = 3 if args.warmup is None else args.warmup
     for _ in range(args.warmup):
         time.sleep(0.001)
     barrier()
@@ -628,7 +647,8 @@ def dry_run(args, world, rank, dist):
 
 def main():
     args = parse()
-    args.warmup = max(args.warmup, 1)
+    if args.warmup is not None:
+        args.warmup = max(args.warmup, 1)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -695,8 +715,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
+    warm(step, args, dev)
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)

@@ -13,7 +13,7 @@ for v in ${VARIANTS:-base}; do
   fi
   RSP_LIB=$lib timeout -k 10 120 python tools/pc_bench.py --cpis ${CPIS:-16 64} --iters 20 ${PC_ARGS:-} 2>&1 | grep -v amdgpu.ids || exit 1
   for i in $(seq ${BENCH_REPS:-1}); do
-    RSP_LIB=$lib timeout -k 10 200 python bench.py --steps 10 --warmup 2 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/ab/$v.json 2>/dev/null || exit $?
+    RSP_LIB=$lib timeout -k 10 200 python bench.py --steps 10 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/ab/$v.json 2>/dev/null || exit $?
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print('bench', d['value'], {k: v['avg_us'] for k, v in r.get('kernels', {}).items()})" gpurun_out/ab/$v.json
   done
 done

@@ -5,7 +5,7 @@ over the timed steps (the last `steps` x launches-per-step chain launches).  In-
 (PC beside PC, MTD beside MTD) pair two kernels that want the same resource; PC beside MTD
 pairs the compute-heavier one with the stream-heavier one.
 
-Usage: lane_overlap.py <kernel_trace.csv> --steps K --warmup W [--json out.json]
+Usage: lane_overlap.py <kernel_trace.csv> --steps K (--warmup W | --warmup-from bench.log) [--json out.json]
 """
 import collections
 import csv
@@ -21,7 +21,11 @@ OURS = {"pc_kernel": "PC", "mtd_kernel": "MTD", "cfar_r_kernel": "CFAR_R", "cfar
 def main():
     a = sys.argv[1:]
     steps = int(a[a.index("--steps") + 1])
-    warmup = int(a[a.index("--warmup") + 1])
+    if "--warmup-from" in a:   # the warmup count bench.py chose (its JSON line's "warmup")
+        line = [ln for ln in open(a[a.index("--warmup-from") + 1]) if ln.startswith("{")][-1]
+        warmup = int(json.loads(line)["warmup"])
+    else:
+        warmup = int(a[a.index("--warmup") + 1])
     rows = []
     for r in csv.DictReader(open(a[0])):
         k = OURS.get(short(r["Kernel_Name"]))

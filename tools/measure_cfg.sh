@@ -12,21 +12,21 @@ EXTRA="$*"
 OUT="$ROOT/gpurun_out/$CFG"; rm -rf "$OUT"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 STEPS=${STEPS:-10}
-timeout -k 10 300 python bench.py --config $CFG --steps $STEPS --warmup 2 --cpu-seconds ${CPU_SECONDS:-10} $EXTRA \
+timeout -k 10 300 python bench.py --config $CFG --steps $STEPS --cpu-seconds ${CPU_SECONDS:-10} $EXTRA \
     > "$OUT/bench.log" 2> "$OUT/bench.err" || { echo "bench rc=$?"; tail -5 "$OUT/bench.err"; exit 1; }
 tail -1 "$OUT/bench.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$CFG', d['value'], d['unit'], 'ms/step', d['ms_per_step'], 'frac', r['frac'], {k: (v['avg_us'], v.get('frac')) for k, v in r.get('kernels', {}).items()})"
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python3 "$ROOT/bench.py" --config $CFG --steps 5 --warmup 1 --cpu-seconds 0 --no-profile $EXTRA > "$OUT/prof.log" 2>&1) \
+    python3 "$ROOT/bench.py" --config $CFG --steps 5 --cpu-seconds 0 --no-profile $EXTRA > "$OUT/prof.log" 2>&1) \
     || { echo "rocprof rc=$?"; tail -3 "$OUT/prof.log"; exit 1; }
-python tools/trace_summary.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/trace.json" > /dev/null
+python tools/trace_summary.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup-from "$OUT/prof.log" --json "$OUT/trace.json" > /dev/null
 python -c "import json; d=json.load(open('$OUT/trace.json')); print('trace span ms/step', d['span_ms_per_step'], {k: v['avg_us'] for k, v in d['kernels'].items()})"
-python tools/lane_overlap.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/overlap.json" > /dev/null || true
+python tools/lane_overlap.py "$OUT/prof/run_kernel_trace.csv" --steps 5 --warmup-from "$OUT/prof.log" --json "$OUT/overlap.json" > /dev/null || true
 # the same on ONE pipeline (--streams 1): kernels do not overlap, so rocprof's per-kernel averages
 # are comparable with bench.py's single-pipeline per-kernel entries
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof1" -o run -- \
-    python3 "$ROOT/bench.py" --config $CFG --steps 5 --warmup 1 --cpu-seconds 0 --no-profile --streams 1 $EXTRA > "$OUT/prof1.log" 2>&1) \
+    python3 "$ROOT/bench.py" --config $CFG --steps 5 --cpu-seconds 0 --no-profile --streams 1 $EXTRA > "$OUT/prof1.log" 2>&1) \
     || { echo "rocprof (1 pipeline) rc=$?"; tail -3 "$OUT/prof1.log"; exit 1; }
-python tools/trace_summary.py "$OUT/prof1/run_kernel_trace.csv" --steps 5 --warmup 1 --json "$OUT/trace_1lane.json" > /dev/null
+python tools/trace_summary.py "$OUT/prof1/run_kernel_trace.csv" --steps 5 --warmup-from "$OUT/prof1.log" --json "$OUT/trace_1lane.json" > /dev/null
 python -c "import json; d=json.load(open('$OUT/trace_1lane.json')); print('1-pipeline trace', d['span_ms_per_step'], {k: v['avg_us'] for k, v in d['kernels'].items()})"
 [ "${PMC:-1}" = "1" ] || exit 0
 PSTEPS=${PMC_STEPS:-2}

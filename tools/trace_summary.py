@@ -4,7 +4,7 @@ kernels: per-kernel launches / mean / total duration, and the device span of the
 (the last `steps` x launches-per-step chain launches), to set beside bench.py's own
 ms_per_step and roofline.
 
-Usage: trace_summary.py <run_kernel_trace.csv> --steps K --warmup W [--json out.json]
+Usage: trace_summary.py <run_kernel_trace.csv> --steps K (--warmup W | --warmup-from bench.log) [--json out.json]
 """
 import collections
 import csv
@@ -21,7 +21,11 @@ def main():
     a = sys.argv[1:]
     path = a[0]
     steps = int(a[a.index("--steps") + 1])
-    warmup = int(a[a.index("--warmup") + 1])
+    if "--warmup-from" in a:   # the warmup count bench.py chose (its JSON line's "warmup")
+        line = [ln for ln in open(a[a.index("--warmup-from") + 1]) if ln.startswith("{")][-1]
+        warmup = int(json.loads(line)["warmup"])
+    else:
+        warmup = int(a[a.index("--warmup") + 1])
     rows = []
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
