@@ -24,32 +24,31 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 // emit the negation modifiers on its own (it spends v_xor + v_mov per rotation), hence the
 // inline asm; -DRSP_NO_ASM selects the portable forms.
 #ifndef RSP_NO_ASM
-// Plain add/sub as packed asm too: left to itself the SLP vectorizer pairs lanes of
-// *different* complex values, (a.x + b.x, c.x + d.x), and then shuffles them back with
-// v_mov into the (re, im) pairs the other primitives take.
+// Plain add/sub as 2-wide vector arithmetic: one v_pk_add_f32 each (the subtraction's
+// negation folds into neg_lo/neg_hi).  Written on scalar halves, the SLP vectorizer pairs
+// lanes of *different* complex values and shuffles them back with v_mov; written as asm,
+// every dependent pair of statements costs an s_nop (see cmul).
+typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) {
-    float2 d;
-    asm("v_pk_add_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-    return d;
+    return __builtin_bit_cast(float2, __builtin_bit_cast(v2f, a) + __builtin_bit_cast(v2f, b));
 }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) {
-    float2 d;
-    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
-    return d;
+    return __builtin_bit_cast(float2, __builtin_bit_cast(v2f, a) - __builtin_bit_cast(v2f, b));
 }
-// a + (-j) b = (a.x + b.y, a.y - b.x)
+// a + (-j) b = (a.x + b.y, a.y - b.x): one v_pk_fma_f32 of the swapped b times (1, -1) --
+// the products by +-1 are exact, so the fma rounds exactly as the add (the constant pair
+// lives in SGPRs; hipcc does not fold a per-half negation into neg_lo/neg_hi itself).
 __device__ __forceinline__ float2 add_mj(float2 a, float2 b) {
-    float2 d;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
-    return d;
+    const v2f bs = __builtin_shufflevector(__builtin_bit_cast(v2f, b), __builtin_bit_cast(v2f, b), 1, 0);
+    return __builtin_bit_cast(float2, __builtin_elementwise_fma(bs, (v2f){1.f, -1.f}, __builtin_bit_cast(v2f, a)));
 }
 // a + j b = (a.x - b.y, a.y + b.x)
 __device__ __forceinline__ float2 add_pj(float2 a, float2 b) {
-    float2 d;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(d) : "v"(a), "v"(b));
-    return d;
+    const v2f bs = __builtin_shufflevector(__builtin_bit_cast(v2f, b), __builtin_bit_cast(v2f, b), 1, 0);
+    return __builtin_bit_cast(float2, __builtin_elementwise_fma(bs, (v2f){-1.f, 1.f}, __builtin_bit_cast(v2f, a)));
 }
 // a * b in two instructions: m = (-a.y b.y, a.y b.x); d = (a.x b.x, a.x b.y) + m
+// (hipcc builds m from a negated copy and a v_mov shuffle: four instructions)
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     float2 m, d;
     asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]" : "=v"(m) : "v"(a), "v"(b));
@@ -63,6 +62,34 @@ __device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(b), "v"(m));
     return d;
 }
+// Two independent complex products in one asm statement, interleaved (mul0 mul1 fma0 fma1):
+// gfx950 needs one wait state between a packed-FP32 result and a VALU that reads it, which
+// hipcc pays as an s_nop after every asm statement whose result the next one reads -- 245 of
+// the PC kernel's 418 nops sat inside cmul.  Interleaved, each fma is one instruction behind
+// its mul.  m0, m1, d0 are early-clobber (written before the inputs' last reads).
+__device__ __forceinline__ void cmul2(float2& d0, float2 a0, float2 b0, float2& d1, float2 a1, float2 b1) {
+    float2 m0, m1, e0, e1;
+    asm("v_pk_mul_f32 %2, %4, %5 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]\n\t"
+        "v_pk_mul_f32 %3, %6, %7 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]\n\t"
+        "v_pk_fma_f32 %0, %4, %5, %2 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %1, %6, %7, %3 op_sel_hi:[0,1,1]"
+        : "=&v"(e0), "=v"(e1), "=&v"(m0), "=&v"(m1)
+        : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+    d0 = e0;
+    d1 = e1;
+}
+// conj(a0 * b0), conj(a1 * b1), as cmul2
+__device__ __forceinline__ void cmul2_conj(float2& d0, float2 a0, float2 b0, float2& d1, float2 a1, float2 b1) {
+    float2 m0, m1, e0, e1;
+    asm("v_pk_mul_f32 %2, %4, %5 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]\n\t"
+        "v_pk_mul_f32 %3, %6, %7 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]\n\t"
+        "v_pk_fma_f32 %0, %4, %5, %2 op_sel_hi:[0,1,1] neg_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %1, %6, %7, %3 op_sel_hi:[0,1,1] neg_hi:[1,0,1]"
+        : "=&v"(e0), "=v"(e1), "=&v"(m0), "=&v"(m1)
+        : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+    d0 = e0;
+    d1 = e1;
+}
 #else
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -72,6 +99,14 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) { return cconj(cmul(a, b)); }
+__device__ __forceinline__ void cmul2(float2& d0, float2 a0, float2 b0, float2& d1, float2 a1, float2 b1) {
+    d0 = cmul(a0, b0);
+    d1 = cmul(a1, b1);
+}
+__device__ __forceinline__ void cmul2_conj(float2& d0, float2 a0, float2 b0, float2& d1, float2 a1, float2 b1) {
+    d0 = cmul_conj(a0, b0);
+    d1 = cmul_conj(a1, b1);
+}
 #endif
 // a * (-j)
 __device__ __forceinline__ float2 cmul_mj(float2 a) { return make_float2(a.y, -a.x); }
@@ -125,8 +160,7 @@ __device__ __forceinline__ void dft8(float2* v) {
     dft4(e0, e1, e2, e3);
     dft4(o0, o1, o2, o3);
     // o_k *= W8^k (W8^2 = -j folded into the adds)
-    o1 = cmul(o1, make_float2(h, -h));
-    o3 = cmul(o3, make_float2(-h, -h));
+    cmul2(o1, o1, make_float2(h, -h), o3, o3, make_float2(-h, -h));
     v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
     v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
     v[2] = add_mj(e2, o2); v[6] = add_pj(e2, o2);
@@ -141,15 +175,11 @@ __device__ __forceinline__ void dft16(float2* v) {
     for (int n2 = 0; n2 < 4; ++n2) dft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
     // v[4*k1 + n2] now holds b[n2][k1]; multiply by W16^(n2*k1)
     // n2=1: k1=1..3 -> W^1, W^2, W^3 ; n2=2: W^2, W^4, W^6 ; n2=3: W^3, W^6, W^9
-    v[5] = cmul(v[5], make_float2(c1, -s1));
-    v[9] = cmul(v[9], make_float2(h, -h));
-    v[13] = cmul(v[13], make_float2(s1, -c1));
-    v[6] = cmul(v[6], make_float2(h, -h));
+    cmul2(v[5], v[5], make_float2(c1, -s1), v[9], v[9], make_float2(h, -h));
+    cmul2(v[13], v[13], make_float2(s1, -c1), v[6], v[6], make_float2(h, -h));
     // v[10] *= W16^4 = -j: folded into dft4_a2mj below
-    v[14] = cmul(v[14], make_float2(-h, -h));
-    v[7] = cmul(v[7], make_float2(s1, -c1));
-    v[11] = cmul(v[11], make_float2(-h, -h));
-    v[15] = cmul(v[15], make_float2(-c1, s1));
+    cmul2(v[14], v[14], make_float2(-h, -h), v[7], v[7], make_float2(s1, -c1));
+    cmul2(v[11], v[11], make_float2(-h, -h), v[15], v[15], make_float2(-c1, s1));
     // second stage: for each k1, DFT4 over n2 of v[4*k1 + n2] -> X[k1 + 4*k2]
     float2 x[16];
 #pragma unroll
@@ -400,33 +430,32 @@ __device__ __forceinline__ void tw_apply(float2* v, const float2* w) {
         // out of a row loop into registers (which would undo the saving)
         float2 w1 = w[0], w4 = w[1];
         asm volatile("" : "+v"(w1), "+v"(w4));
-        const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w8 = cmul(w4, w4), w12 = cmul(w8, w4);
-        v[1] = cmul(v[1], w1);
-        v[2] = cmul(v[2], w2);
-        v[3] = cmul(v[3], w3);
-        v[4] = cmul(v[4], w4);
-        v[5] = cmul(v[5], cmul(w4, w1));
-        v[6] = cmul(v[6], cmul(w4, w2));
-        v[7] = cmul(v[7], cmul(w4, w3));
-        v[8] = cmul(v[8], w8);
-        v[9] = cmul(v[9], cmul(w8, w1));
-        v[10] = cmul(v[10], cmul(w8, w2));
-        v[11] = cmul(v[11], cmul(w8, w3));
-        v[12] = cmul(v[12], w12);
-        v[13] = cmul(v[13], cmul(w12, w1));
-        v[14] = cmul(v[14], cmul(w12, w2));
-        v[15] = cmul(v[15], cmul(w12, w3));
+        // the same products as before, paired so each pair's inputs were formed >= 1 pair earlier
+        float2 w2, w3, w8, w12, p5, p6, p7, p9, p10, p11, p13, p14, p15;
+        cmul2(w2, w1, w1, w8, w4, w4);
+        cmul2(w3, w2, w1, w12, w8, w4);
+        cmul2(v[1], v[1], w1, v[2], v[2], w2);
+        cmul2(v[3], v[3], w3, p5, w4, w1);
+        cmul2(v[4], v[4], w4, p6, w4, w2);
+        cmul2(v[5], v[5], p5, p7, w4, w3);
+        cmul2(v[6], v[6], p6, p9, w8, w1);
+        cmul2(v[7], v[7], p7, p10, w8, w2);
+        cmul2(v[8], v[8], w8, p11, w8, w3);
+        cmul2(v[9], v[9], p9, p13, w12, w1);
+        cmul2(v[10], v[10], p10, p14, w12, w2);
+        cmul2(v[11], v[11], p11, p15, w12, w3);
+        cmul2(v[12], v[12], w12, v[13], v[13], p13);
+        cmul2(v[14], v[14], p14, v[15], v[15], p15);
     } else if constexpr (R == 8) {
         float2 w1 = w[0], w4 = w[1];
         asm volatile("" : "+v"(w1), "+v"(w4));
-        const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-        v[1] = cmul(v[1], w1);
-        v[2] = cmul(v[2], w2);
-        v[3] = cmul(v[3], w3);
-        v[4] = cmul(v[4], w4);
-        v[5] = cmul(v[5], cmul(w4, w1));
-        v[6] = cmul(v[6], cmul(w4, w2));
-        v[7] = cmul(v[7], cmul(w4, w3));
+        float2 w2, w3, p5, p6, p7;
+        cmul2(w2, w1, w1, p5, w4, w1);
+        cmul2(w3, w2, w1, v[1], v[1], w1);
+        cmul2(v[2], v[2], w2, p6, w4, w2);
+        cmul2(v[3], v[3], w3, p7, w4, w3);
+        cmul2(v[4], v[4], w4, v[5], v[5], p5);
+        cmul2(v[6], v[6], p6, v[7], v[7], p7);
     } else {
         float2 w0 = w[0];
         asm volatile("" : "+v"(w0));

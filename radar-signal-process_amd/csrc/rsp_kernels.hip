@@ -395,7 +395,8 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     RSP_STAMP(0, 3, false);
     if constexpr (kEarly) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) u[m] = cmul_conj(u[m], hs[m]);   // conj(X.*H), 1/N in H
+        for (int m = 0; m < E; m += 2)   // conj(X.*H), 1/N in H (E is even)
+            cmul2_conj(u[m], u[m], hs[m], u[m + 1], u[m + 1], hs[m + 1]);
     } else {
         constexpr int HB = 8;
 #pragma unroll
@@ -404,7 +405,8 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
 #pragma unroll
             for (int m = 0; m < HB; ++m) h[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * (m0 + m)) * 8u);
 #pragma unroll
-            for (int m = 0; m < HB; ++m) u[m0 + m] = cmul_conj(u[m0 + m], h[m]);   // conj(X.*H), 1/N in H
+            for (int m = 0; m < HB; m += 2)   // conj(X.*H), 1/N in H
+                cmul2_conj(u[m0 + m], u[m0 + m], h[m], u[m0 + m + 1], u[m0 + m + 1], h[m + 1]);
         }
     }
     RSP_STAMP(0, 4, false);
