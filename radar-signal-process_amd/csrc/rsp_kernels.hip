@@ -1763,10 +1763,79 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits_kernel(const float* __r
     cfar_hit_region<REF, SAVE>(rdm, flag, hits, counts, (int)blockIdx.x, region, a, (int)threadIdx.x, kHitThreads);
 }
 
+// The reference's window (5 reference + 7 guard cells): one wave per hit region, four regions
+// per workgroup.  A region is one MTD tile's hit list (~10-50 hits at c3-c5), so a workgroup
+// per region left most of its threads idle and took one dependent round-trip chain (count ->
+// index -> cells) per region; here the count and the lane's first index load together (the
+// index is in bounds past the count: a region holds W*P >= 256 entries), the lane's 27 cells
+// follow as one batch of range-checked buffer loads (RangeJob57's gathers), and hits past the
+// first 64 of a region take the generic per-hit loop.
+__global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* __restrict__ rdm,
+                                                                  uint8_t* __restrict__ flag,
+                                                                  const uint32_t* __restrict__ hits,
+                                                                  const uint32_t* __restrict__ counts, int nregions,
+                                                                  int region, CfarRArgs a) {
+    const int rg = (int)(blockIdx.x * (kHitThreads / 64) + threadIdx.x / 64);
+    if (rg >= nregions) return;   // (wave-uniform; no barriers below)
+    const int k = (int)(threadIdx.x % 64);
+    constexpr int H = RangeJob57::H, NX = RangeJob57::NX;
+    const uint32_t n = counts[rg];
+    const uint32_t idx = hits[(size_t)rg * region + k];
+    const bool mine = (uint32_t)k < n;
+    const uint32_t R = (uint32_t)a.R, V = (uint32_t)a.V;
+    const uint32_t row = idx / R;
+    const int r = (int)(idx - row * R);
+    const int v = (int)(row % V);
+    const bool zrow = v >= a.cz_lo && v < a.cz_hi;
+    const auto rr = buf_rsrc(rdm, kOob);
+    float x[NX];
+#pragma unroll
+    for (int q = 0; q < NX; ++q) {
+        const int c = r - H + q;
+        const bool ok = mine && !zrow && c >= 0 && c < a.R;
+        x[q] = buf_ld_f(rr, ok ? (row * R + (uint32_t)c) * 4u : kOob, 0u);
+    }
+    if (mine) {
+        int slo, shi;
+        seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
+        if (shi > slo) {
+            int best = -1;
+            float bx = 0.f;
+#pragma unroll
+            for (int e = -1; e <= 1; ++e) {
+                const int q = r + e, i = H + e;   // x[i] = cell q
+                float sl = 0.f, sr = 0.f;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    sl += x[i - 12 + j];
+                    sr += x[i + 8 + j];
+                }
+                const bool lok = q - 12 >= slo, rok = q + 12 < shi;
+                const float xq = x[i];
+                if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
+                    best = q;
+                    bx = xq;
+                }
+            }
+            if (best >= 0) flag[(size_t)row * R + best] = 1;
+        }
+    }
+    if (n > 64u) cfar_hit_region<5, 7>(rdm, flag, hits, counts, rg, region, a, 64 + k, 64);
+}
+
 hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
                             int nregions, int region, const CfarRArgs& a, hipStream_t s) {
     if (nregions <= 0) return hipSuccess;
-    if (a.ref == 5 && a.save == 7)   // the reference's parameters
+    // (the chunk's RDM holds nregions * region cells: byte offsets stay below the range check).
+    // Hits per region grow with the tile's pulse count: regions of up to 4096 cells (c3: ~10
+    // hits, c4: ~50) take a wave each (c4: 44 -> 31 us per launch, c3 unchanged); the 8192-cell
+    // regions of P = 512 (c5: ~460 hits) keep a workgroup each (a wave took 12 -> 22 us).
+    if (a.ref == 5 && a.save == 7 && region >= 64 && region <= 4096 &&
+        (uint64_t)nregions * (uint64_t)region < (uint64_t)(kOob / 4u)) {
+        constexpr int RPB = kHitThreads / 64;
+        hipLaunchKernelGGL(cfar_hits57_kernel, dim3((unsigned)((nregions + RPB - 1) / RPB)), dim3(kHitThreads), 0, s,
+                           rdm, flag, hits, counts, nregions, region, a);
+    } else if (a.ref == 5 && a.save == 7)   // the reference's parameters
         hipLaunchKernelGGL((cfar_hits_kernel<5, 7>), dim3((unsigned)nregions), dim3(kHitThreads), 0, s, rdm, flag,
                            hits, counts, nregions, region, a);
     else
