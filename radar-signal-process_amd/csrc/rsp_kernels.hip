@@ -1168,7 +1168,10 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
         // their partial RDM / flag lines (W = 16: 64-B RDM and 16-B flag row segments at c5)
         // meet in one L2 and leave it merged (c5 +1.5-2 %; at W = 32 the RDM segments are whole
         // 128-B lines and the grouping cost c3's MTD 3 %)
-        constexpr int K = 4;
+#ifndef RSP_DIAG_MTD_XCD_K   // dev-only diagnostic build: consecutive narrow tiles per XCD
+#define RSP_DIAG_MTD_XCD_K 4
+#endif
+        constexpr int K = RSP_DIAG_MTD_XCD_K;
         const int x = bx;
         if (gx % (8 * K) == 0) T.bx = (x / (8 * K)) * (8 * K) + (x % 8) * K + (x / 8) % K;
     }

@@ -204,6 +204,41 @@ def test_chain_cfar_variants(torch_cuda, methodV, methodR, ref_n, guard, P, R):
     eng.close()
 
 
+@pytest.mark.parametrize("P,R,W", [(128, 4096, 32), (256, 2048, 16), (512, 2048, 16)])
+def test_dense_hit_regions_range_stage(torch_cuda, P, R, W):
+    """The range stage of executeCFAR.m:45-84 on dense hit regions: thresholds of 1.5 make most
+    tiles carry more than 64 Doppler hits, so the wave-per-region range kernel (regions of
+    <= 4096 cells: its first-64 batch and its per-hit tail loop) and the workgroup-per-region
+    one (P = 512) both run past their first pass; flags against the oracle as above."""
+    torch = torch_cuda
+    import dataclasses
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    spec = presets.v2(P, R)
+    cf = dataclasses.replace(presets.default_cfar(spec), TV=1.5, TR=1.5)
+    eng = Engine(spec, device=0)
+    echo = synth.echo_numpy(spec, 2, seed=3000 + P)
+    d_in = torch.from_numpy(echo).cuda()
+    shp = (2, P, R)
+    d_rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    d_fv = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm, flag=d_flag, flagV=d_fv, cfar=cf)
+    torch.cuda.synchronize()
+    rdm = oracle_rdm("v2", echo)
+    assert rel_err(d_rdm.cpu().numpy(), rdm) < RDM_TOL
+    flag, flagV, amb = oracle_flags_c(rdm, cf)
+    # hits per MTD tile (W range bins x all Doppler rows): the dense case this test is about
+    per_tile = flagV.reshape(2, P, R // W, W).sum(axis=(1, 3))
+    assert (per_tile > 64).mean() > 0.5, per_tile.max()
+    hard, soft = flag_mismatch(d_flag.cpu().numpy(), flag, amb)
+    hardv, softv = flag_mismatch(d_fv.cpu().numpy(), flagV, amb)
+    assert hard == 0 and hardv == 0, (hard, hardv)
+    assert soft <= 8 and softv <= 8, (soft, softv)
+    assert flag.sum() > 0
+    eng.close()
+
+
 # ---------------------------------------------------------------- c5: fp16 I/Q at 512 x 16384
 def _fp16_run(torch, eng, echo, cf):
     from rsp import synth

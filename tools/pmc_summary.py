@@ -17,7 +17,7 @@ import sys
 # kernel-name fragment -> the bench's kernel label (rsp_profile ids)
 LABELS = (("pc_persist_kernel", "pc_kernel"), ("pc_mf_kernel", "pc_kernel"), ("pc_kernel", "pc_kernel"),
           ("mtd_bluestein_kernel", "mtd_kernel"), ("mtd_kernel", "mtd_kernel"),
-          ("cfar_hits_kernel", "cfar_r_kernel"), ("cfar_r16_kernel", "cfar_r_kernel"),
+          ("cfar_hits_kernel", "cfar_r_kernel"), ("cfar_hits57_kernel", "cfar_r_kernel"), ("cfar_r16_kernel", "cfar_r_kernel"),
           ("cfar_r_kernel", "cfar_r_kernel"), ("cfar_r_generic_kernel", "cfar_r_kernel"),
           ("cfar_v_kernel", "cfar_v_kernel"), ("fillBuffer", "flag_memset"), ("hits_kernel", "hits_kernel"),
           ("measure_kernel", "measure_kernel"), ("prefilter_kernel", "prefilter_kernel"), ("mti_chain_kernel", "mti_chain_kernel"),
