@@ -1164,16 +1164,15 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
     T.cell_base = (uint32_t)(cpi * plane);
     T.bx = bx;
-    if constexpr (C::W < 32) {   // 4 consecutive tiles on one XCD (workgroup x goes to XCD x % 8):
-        // their partial RDM / flag lines (W = 16: 64-B RDM and 16-B flag row segments at c5)
-        // meet in one L2 and leave it merged (c5 +1.5-2 %; at W = 32 the RDM segments are whole
-        // 128-B lines and the grouping cost c3's MTD 3 %)
-#ifndef RSP_DIAG_MTD_XCD_K   // dev-only diagnostic build: consecutive narrow tiles per XCD
-#define RSP_DIAG_MTD_XCD_K 4
-#endif
-        constexpr int K = RSP_DIAG_MTD_XCD_K;
+    if constexpr (C::W < 32) {   // 8 consecutive tiles on one XCD (workgroup x goes to XCD x % 8):
+        // their partial RDM / flag row segments (W = 16: 64-B RDM and 16-B flag segments) meet
+        // in one L2 and leave it as whole lines -- 8 tiles make the flag segments whole 128-B
+        // lines too (c4 MTD 419 -> 397 us per launch, c4 +4.7 %; c5 neutral; 4 tiles: c5 +1.5-2 %
+        // over none); 4 tiles when the row's tile count is not a multiple of 64.  (At W = 32 the
+        // RDM segments are whole lines and grouping cost c3's MTD 3 %.)
         const int x = bx;
-        if (gx % (8 * K) == 0) T.bx = (x / (8 * K)) * (8 * K) + (x % 8) * K + (x / 8) % K;
+        if (gx % 64 == 0) T.bx = (x / 64) * 64 + (x % 8) * 8 + (x / 8) % 8;
+        else if (gx % 32 == 0) T.bx = (x / 32) * 32 + (x % 8) * 4 + (x / 8) % 4;
     }
     const int nwg = gx * gy;
     // one instance of the tile (the kernel's code stays ~half the size: it shares the
