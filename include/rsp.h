@@ -176,7 +176,8 @@ const char* rsp_last_error(const rsp_ctx* ctx);
 /* CPIs processed per internal chunk (PC scratch = chunk * P * R_out * 8 bytes, sized to
  * stay in the 256 MiB Infinity Cache).  0 restores the default.  Window mode counts output
  * windows: chunk / windows frame pairs per chunk (each chunk also pulse-compresses one
- * look-ahead frame); the default there is at least 16 pairs. */
+ * look-ahead frame); the default there is at least 32 pairs (fewer look-ahead frames and
+ * launches beat Infinity-Cache residency for the window stream). */
 int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 
 /* Number of chunk pipelines (1..4; 0 = the default: 2, window mode 1): chunk k runs on the

@@ -903,18 +903,19 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     for (int i = 0; i < win; ++i) m.win_start[i] = (int)mround((double)i * P / win);
     int64_t cu = chunk_of(ctx, units * ocpi);              // CPIs per chunk
     // Default pipelines: 2 (PC of one chunk overlaps MTD / CFAR of the other); window mode 1 with
-    // chunks of >= 16 frame pairs (look-ahead PC overhead <= 1/16): c4 98-99k windows/s against
-    // 94k with 2 pipelines of 8 pairs, whose 2 x 144 MiB of scratch overflows the Infinity Cache
+    // chunks of >= 32 frame pairs (look-ahead PC overhead <= 1/32, fewer launch tails): c4 114.9k
+    // windows/s against 111.9k at 16 pairs and 106.5k at 8 (round 3); two pipelines of 8 pairs
+    // lost (2 x 144 MiB of scratch overflows the Infinity Cache)
     const int nsd = ctx->nstreams > 0 ? ctx->nstreams : (win > 0 ? 1 : 2);
     if (win > 0) {
         cu = cu / ocpi;
         if (ctx->chunk > 0) {
             cu = cu > 0 ? cu : 1;                          // explicit chunk (rsp_set_chunk): as asked
-        } else if (cu < 16) {
-            // at least 16 pairs, but never more cells per chunk slot than the 32-bit hit
+        } else if (cu < 32) {
+            // at least 32 pairs, but never more cells per chunk slot than the 32-bit hit
             // indices address (down to the old minimum and below for the largest windows)
             const int64_t fit = (int64_t)(0xffffffffull / ((uint64_t)ocpi * (uint64_t)V * (uint64_t)Ro));
-            cu = 16 < fit ? 16 : (fit > cu ? fit : cu);
+            cu = 32 < fit ? 32 : (fit > cu ? fit : cu);
             if (cu < 1) cu = 1;
         }
     }
