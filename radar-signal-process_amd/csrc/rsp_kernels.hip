@@ -721,28 +721,28 @@ __device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t 
         for (int i = 0; i < N; ++i) buf_st_u8(0, o.fl, o.vo, (uint32_t)i * o.R);
     }
     if (__ballot(mask != 0u) == 0) return;   // the common case: no hit in the wave's rows
-    // dense rows (the 0-v band edges fire in every column): one wave-wide prefix sum of the
-    // lanes' hit counts and one LDS atomic per wave, then each lane writes its run of entries
-    const int lane = __lane_id();
-    const uint32_t cnt = (uint32_t)__popc(mask);
-    uint32_t incl = cnt;
+    // row by row: one ballot per row of the run gives the row's hit lanes, so the wave's
+    // entries go out row-major -- each store instruction writes the row's hits as one
+    // contiguous run (a lane-major run per lane made every store a scatter), and neighbouring
+    // entries are neighbouring columns of one row, whose 27-cell range windows overlap.  The
+    // counts are scalar (popcounts of the ballots): one LDS atomic per wave, no shuffles.
+    uint32_t total = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
-    }
-    const uint32_t total = __shfl(incl, 63);
+    for (int i = 0; i < N; ++i) total += (uint32_t)__popcll(__ballot((mask >> i) & 1u));
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(o.lds_count, total);
+    if (__lane_id() == 0) base = atomicAdd(o.lds_count, total);
     base = __shfl(base, 0);
-    uint32_t* dst = o.hits + base + (incl - cnt);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
+        const uint64_t b = __ballot((mask >> i) & 1u);
+        if (b == 0) continue;   // (wave-uniform)
         if ((mask >> i) & 1u) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            uint32_t* dst = o.hits + base + below;
             if (o.coherent) st_u32_sc1(dst, o.cell0 + (uint32_t)i * o.R);
             else *dst = o.cell0 + (uint32_t)i * o.R;
-            ++dst;
         }
+        base += (uint32_t)__popcll(b);
     }
 }
 
