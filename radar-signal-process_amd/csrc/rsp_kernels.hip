@@ -1771,7 +1771,7 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits_kernel(const float* __r
 // index -> cells) per region; here the count and the lane's first index load together (the
 // index is in bounds past the count: a region holds W*P >= 256 entries), the lane's 27 cells
 // follow as one batch of range-checked buffer loads (RangeJob57's gathers), and hits past the
-// first 64 of a region take the generic per-hit loop.
+// first 64 of a region follow in further batches of 64 the same way.
 __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* __restrict__ rdm,
                                                                   uint8_t* __restrict__ flag,
                                                                   const uint32_t* __restrict__ hits,
@@ -1781,48 +1781,55 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* _
     if (rg >= nregions) return;   // (wave-uniform; no barriers below)
     const int k = (int)(threadIdx.x % 64);
     constexpr int H = RangeJob57::H, NX = RangeJob57::NX;
+    const uint32_t* list = hits + (size_t)rg * region;
     const uint32_t n = counts[rg];
-    const uint32_t idx = hits[(size_t)rg * region + k];
-    const bool mine = (uint32_t)k < n;
+    uint32_t idx = list[k];
     const uint32_t R = (uint32_t)a.R, V = (uint32_t)a.V;
-    const uint32_t row = idx / R;
-    const int r = (int)(idx - row * R);
-    const int v = (int)(row % V);
-    const bool zrow = v >= a.cz_lo && v < a.cz_hi;
     const auto rr = buf_rsrc(rdm, kOob);
-    float x[NX];
+    // batches of 64 hits, one per lane; the next batch's index is loaded before this batch's
+    // cells, so its round trip overlaps the gathers
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const bool mine = b0 + (uint32_t)k < n;
+        const uint32_t nk = b0 + 64u + (uint32_t)k;
+        const uint32_t next = nk < n ? list[nk] : 0u;
+        const uint32_t row = idx / R;
+        const int r = (int)(idx - row * R);
+        const int v = (int)(row % V);
+        const bool zrow = v >= a.cz_lo && v < a.cz_hi;
+        float x[NX];
 #pragma unroll
-    for (int q = 0; q < NX; ++q) {
-        const int c = r - H + q;
-        const bool ok = mine && !zrow && c >= 0 && c < a.R;
-        x[q] = buf_ld_f(rr, ok ? (row * R + (uint32_t)c) * 4u : kOob, 0u);
-    }
-    if (mine) {
-        int slo, shi;
-        seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
-        if (shi > slo) {
-            int best = -1;
-            float bx = 0.f;
-#pragma unroll
-            for (int e = -1; e <= 1; ++e) {
-                const int q = r + e, i = H + e;   // x[i] = cell q
-                float sl = 0.f, sr = 0.f;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    sl += x[i - 12 + j];
-                    sr += x[i + 8 + j];
-                }
-                const bool lok = q - 12 >= slo, rok = q + 12 < shi;
-                const float xq = x[i];
-                if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
-                    best = q;
-                    bx = xq;
-                }
-            }
-            if (best >= 0) flag[(size_t)row * R + best] = 1;
+        for (int q = 0; q < NX; ++q) {
+            const int c = r - H + q;
+            const bool ok = mine && !zrow && c >= 0 && c < a.R;
+            x[q] = buf_ld_f(rr, ok ? (row * R + (uint32_t)c) * 4u : kOob, 0u);
         }
+        if (mine) {
+            int slo, shi;
+            seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
+            if (shi > slo) {
+                int best = -1;
+                float bx = 0.f;
+#pragma unroll
+                for (int e = -1; e <= 1; ++e) {
+                    const int q = r + e, i = H + e;   // x[i] = cell q
+                    float sl = 0.f, sr = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        sl += x[i - 12 + j];
+                        sr += x[i + 8 + j];
+                    }
+                    const bool lok = q - 12 >= slo, rok = q + 12 < shi;
+                    const float xq = x[i];
+                    if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
+                        best = q;
+                        bx = xq;
+                    }
+                }
+                if (best >= 0) flag[(size_t)row * R + best] = 1;
+            }
+        }
+        idx = next;
     }
-    if (n > 64u) cfar_hit_region<5, 7>(rdm, flag, hits, counts, rg, region, a, 64 + k, 64);
 }
 
 hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
