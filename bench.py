@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on device 0, gloo collectives (value not a result)")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher test hook
+    # test hook: every rank on this device WITHOUT --share-device (the duplicate-device guard must fire);
+    # in --dry-run, a fake device identity shared by all ranks
+    ap.add_argument("--force-device", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="--gpus N launcher: seconds before the ranks are stopped")
     args = ap.parse_args()
@@ -605,6 +608,51 @@ def warm(step, args, dev):
     args.warmup = n
 
 
+def device_identity(local, dry=False, force=-1):
+    """What identifies the GPU this rank drives: the local index, HIP/CUDA_VISIBLE_DEVICES, and
+    from the device properties the UUID and the PCI domain/bus/device (the duplicate-device guard
+    compares these).  --dry-run: a fake identity (all ranks alike under --force-device)."""
+    vis = os.environ.get("HIP_VISIBLE_DEVICES", os.environ.get("CUDA_VISIBLE_DEVICES"))
+    if dry:
+        return {"local": local, "visible": vis, "uuid": "dry-run-%d" % (force if force >= 0 else local),
+                "pci": None, "name": "none (dry run)"}
+    import torch
+    pr = torch.cuda.get_device_properties(local)
+    pci = [getattr(pr, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    uuid = getattr(pr, "uuid", None)
+    return {"local": local, "visible": vis, "uuid": str(uuid) if uuid is not None else None,
+            "pci": ("%04x:%02x:%02x" % tuple(pci)) if all(v is not None for v in pci) else None,
+            "name": getattr(pr, "gcnArchName", None) or pr.name}
+
+
+def duplicate_devices(idents):
+    """Pairs of ranks whose identities name one physical GPU (same UUID, or same PCI address)."""
+    dup = []
+    for i in range(len(idents)):
+        for j in range(i + 1, len(idents)):
+            a, b = idents[i], idents[j]
+            if any(a.get(k) is not None and a.get(k) == b.get(k) for k in ("uuid", "pci")):
+                dup.append((i, j))
+    return dup
+
+
+def check_devices(args, world, rank, local, dist):
+    """Gather every rank's device identity over gloo and refuse to run when two ranks drive
+    one GPU without --share-device: n_gpus must count distinct GPUs.  Returns the identities."""
+    ident = device_identity(local, dry=args.dry_run, force=args.force_device)
+    idents = [ident]
+    if world > 1:
+        idents = [None] * world
+        dist.all_gather_object(idents, ident)
+    dup = duplicate_devices(idents)
+    if dup and not args.share_device:
+        i, j = dup[0]
+        raise SystemExit("bench.py: ranks %d and %d drive the same GPU (%s); %d ranks would not be %d GPUs "
+                         "(use --share-device for a one-GPU rehearsal)" % (
+                             i, j, idents[i].get("uuid") or idents[i].get("pci"), world, world))
+    return idents
+
+
 def dry_run(args, world, rank, dist):
     """--dry-run: the multi-rank path without a GPU -- gloo rendezvous, each rank's shard plan,
     a stub step (sleep), barrier + max-over-ranks timing, the per-rank step times and the JSON
@@ -613,6 +661,7 @@ def dry_run(args, world, rank, dist):
     plan = rank_plan(args, rank)
     if rank == args.dry_run_fail_rank:
         raise SystemExit("dry run: rank %d fails on request" % rank)
+    plan["device"] = check_devices(args, world, rank, rank, dist)[rank]
 
     def barrier():
         if world > 1:
@@ -639,7 +688,9 @@ def dry_run(args, world, rank, dist):
             "unit": "window/s" if args.win else "CPI/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(max(per_rank) / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dry_run": True, "config": {"workload": args.config, "batch_per_gpu": args.batch},
-            "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank], "shards": plans}), flush=True)
+            "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank], "shards": plans,
+            "collectives": dist.get_backend() if world > 1 else None,
+            "distinct_devices": len({(p["device"].get("uuid"), p["device"].get("pci")) for p in plans})}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -660,19 +711,23 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
+        # gloo (host) for the timing barrier and the per-rank gathers: the data path exchanges
+        # nothing between GPUs (north_star: frames are independent), so no RCCL communicator
+        # is created at all
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dry_run or args.share_device:
-            dist.init_process_group(backend="gloo")
-        else:
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(backend="gloo")
     if args.dry_run:
         return dry_run(args, world, rank, dist)
     from rsp import presets, shard, synth
     from rsp.engine import Engine
     if args.share_device:
         local = 0
+    elif args.force_device >= 0:
+        local = args.force_device
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    devices = check_devices(args, world, rank, local, dist)
+    args.device_identity = devices[rank]
     if args.config == "ingest":
         return bench_ingest(args, world, rank, local, dev, dist)
     if args.config == "measure":
@@ -693,6 +748,7 @@ def main():
     # contiguous shard of the stream per rank (weak scaling): seed = 1000 + config id + first
     # unit index; window mode also holds the look-ahead frame of its last pair (halo)
     plan = rank_plan(args, rank)
+    plan["device"] = args.device_identity
     if win:
         flo, fhi = plan["frames"]
         echo = synth.echo_torch(spec, fhi - flo, seed=plan["seed"], device=dev, half=args.half)
@@ -867,7 +923,10 @@ def main():
                        "input": "c32f16" if args.half else "c64",
                        "prefilter": "fused iSTC + MTI(30)" if args.prefilter else None,
                        "parallelism": ("%d ranks sharing device 0 (launcher rehearsal, not a scaling result)" % world
-                                       if args.share_device else "frame-sharded x%d, no collective" % world)},
+                                       if args.share_device else "frame-sharded x%d, no data-path collective "
+                                       "(gloo host barrier/gathers only)" % world)},
+            "distinct_devices": len({(d["device"].get("uuid"), d["device"].get("pci")) for d in plans}),
+            "collectives": dist.get_backend() if world > 1 else None,
             "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank],
             "shards": plans,
             "hbm_GBps_per_gpu": round(achieved, 1),

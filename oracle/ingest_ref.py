@@ -201,8 +201,10 @@ class FrameReader:
                 return out, servo, False, True
             if dtype == 0:                                                     # :144-147
                 cur = np.frombuffer(raw[:pdn * ch * 2], dtype="<i2").reshape(pdn, ch).astype(np.float64)
-            elif dtype != 1:                                                   # :130-135,162-164
+            elif dtype == 2:                                                   # :130-135,162-164
                 cur = dbf24_parse(raw, pdn, ch)
+            elif dtype > 2:                                                    # :141 typecast only; no
+                cur = np.zeros((point, beams), dtype=np.complex128)            # switch case (:160-165)
             else:
                 words = np.frombuffer(raw[:pdn * ch * 4], dtype="<i2").astype(np.float64)   # :138,150
                 sd = words.reshape(pdn, ch * 2)                                # :151

@@ -851,6 +851,8 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
 int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_pc_split: null ctx");
     if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "rsp_set_pc_split: CFAR-only context");
+    if (!ctx->pc_v2)   // the generic PC path has no split to select
+        return fail(ctx, RSP_ERR_UNSUPPORTED, "rsp_set_pc_split: this context has no specialised PC path");
     const std::vector<rsp::PcMfArgs>& src = enable ? ctx->pc_mf_split : ctx->pc_mf_whole;
     for (size_t i = 0; i < ctx->pc_mf.size() && i < src.size(); ++i) {
         const float* gain = ctx->pc_mf[i].gain;   // the fused pre-filter stays as set

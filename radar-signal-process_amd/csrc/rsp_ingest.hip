@@ -6,11 +6,13 @@
 //                  (FrameDataRead_xzr.m:149-158);
 //   ADC (type 0)   int16 per channel, the (samples x channels) matrix itself (:144-147), which
 //                  passes the size check only with channel_num == beam_num;
-//   DBF (other)    the 24-bit branch (:130-135,162-164) as MATLAB evaluates it: data_temp is
+//   DBF (type 2)   the 24-bit branch (:130-135,162-164) as MATLAB evaluates it: data_temp is
 //                  uint8, so b0 + b1*2^8 + b2*2^16 saturates (255 once b1 or b2 is non-zero,
 //                  else b0) and the > 2^23 sign fix never fires; value pairs form the I/Q
 //                  columns.  (The reference marks this branch unfinished; its results are
 //                  reproduced as it computes them.)
+//   types 3..255   payload sized as DBF (:110-112) and read, no switch case (:160-165): the row
+//                  is zeros(point_PRT, beam_num), which passes the :171 size check.
 //
 // Two launches per frame, both on the caller's stream:
 //   ingest_check_kernel  one workgroup, a thread per PRT: locates its record, validates the
@@ -79,7 +81,8 @@ __device__ __forceinline__ int32_t check_record(const uint8_t* stream, int64_t n
     bool shape;                                                             // :171-176
     if (h.type == 1u) shape = (int)h.ch == a.channel_num && (int)h.pdn == a.point_prt;   // (and :158's inner dimension)
     else if (h.type == 0u) shape = (int)h.ch == a.beam_num && (int)h.pdn == a.point_prt;
-    else shape = dbf24_values((int)h.ch) == 2 * a.beam_num && (int)h.pdn == a.point_prt;
+    else if (h.type == 2u) shape = dbf24_values((int)h.ch) == 2 * a.beam_num && (int)h.pdn == a.point_prt;
+    else shape = true;   // types 3..255: no switch case matches, the zeros(point_PRT, beam_num) row passes
     if (!shape) return RSP_PRT_BAD_SHAPE;
     if (base + rec > nbytes) {                                              // stored, then :184-189
         *stop = p + 1;
@@ -180,7 +183,11 @@ __global__ __launch_bounds__(256) void ingest_decode_kernel(const uint8_t* __res
         }
         return;
     }
-    if (type != 1) {   // 24-bit DBF branch as MATLAB's uint8 arithmetic evaluates it
+    if (type > 2) {   // types 3..255 (:160-165 has no case): the row stays zeros(point_PRT, beam_num)
+        for (int b = 0; b < a.beam_num; ++b) out[(size_t)b * a.beam_stride + o] = make_float2(0.f, 0.f);
+        return;
+    }
+    if (type == 2) {   // 24-bit DBF branch as MATLAB's uint8 arithmetic evaluates it
         const uint32_t L = (uint32_t)dbf24_row_bytes(a.types[p] >> 8);   // the PRT's own channel count
         const auto pr = buf_rsrc(pay, (uint32_t)a.point_prt * L);
         const uint32_t row = (uint32_t)s * L;

@@ -143,7 +143,10 @@ def dbf24_values(ch):
 
 def _shape_ok(data_type, pdn, ch, cfg):
     """Whether the reference gets past :171-176 (and :158's inner dimension for DDC) -- the host
-    needs it only to stop reading where the reference does (before the tail)."""
+    needs it only to stop reading where the reference does (before the tail).  Types 3..255
+    match no case of :160-165, so their row stays zeros(point_PRT, beam_num) and always passes."""
+    if data_type > 2:
+        return True
     if pdn != cfg["point_PRT"]:
         return False
     if data_type == 1:

@@ -1,7 +1,8 @@
 """Frame sharding across GPUs: CPIs are independent, so each rank owns a
 contiguous range of the CPI stream and no data crosses ranks.  The only collectives are
-the timing barrier and the max-over-ranks of the elapsed time (torch.distributed: RCCL on
-GPUs, gloo in the CPU tests).  In sliding-window mode (config c4) a shard also reads one
+the timing barrier and the per-rank gathers of the elapsed time and the shard plans, all
+over gloo on the host (bench.py creates no RCCL communicator: north_star's "no RCCL
+collective").  In sliding-window mode (config c4) a shard also reads one
 look-ahead frame (halo) owned by the next rank: see window_frames()."""
 
 

@@ -35,6 +35,11 @@ def test_launcher_cpi_shards(world):
     assert all(hi - lo == 5 for lo, hi in spans)                     # weak scaling: 5 CPIs per rank
     assert [s["seed"] for s in out["shards"]] == [1003 + lo for lo, _ in spans]
     assert out["launcher"].startswith("bench.py --gpus %d" % world)
+    # host-side gloo is the only process group (no RCCL communicator on the path), and every
+    # rank records the device it drives
+    assert out["collectives"] == "gloo"
+    assert [s["device"]["local"] for s in out["shards"]] == list(range(world))
+    assert out["distinct_devices"] == world
 
 
 def test_launcher_window_halo():
@@ -62,3 +67,23 @@ def test_world_size_must_match_gpus():
     rc, out, err = _run(["--gpus", "2", "--dry-run", "--steps", "1"], env_extra={"WORLD_SIZE": "1"})
     assert rc == 2 and out is None
     assert "WORLD_SIZE=1 but --gpus 2" in err
+
+
+def test_duplicate_device_guard():
+    """Two ranks that report one physical GPU (here: the dry run's fake identity, all ranks
+    on device 0 without --share-device) make the launch fail instead of printing n_gpus = 2."""
+    rc, out, err = _run(["--gpus", "2", "--dry-run", "--steps", "1", "--warmup", "1", "--force-device", "0",
+                         "--launch-timeout", "120"])
+    assert rc != 0 and out is None
+    assert "drive the same GPU" in err
+
+
+def test_duplicate_device_check_unit():
+    sys.path.insert(0, ROOT)
+    import bench
+    a = {"local": 0, "uuid": "GPU-1", "pci": "0000:05:00"}
+    b = {"local": 1, "uuid": "GPU-2", "pci": "0000:15:00"}
+    assert bench.duplicate_devices([a, b]) == []
+    assert bench.duplicate_devices([a, b, dict(a, local=2)]) == [(0, 2)]
+    assert bench.duplicate_devices([a, dict(b, uuid=None, pci="0000:05:00")]) == [(0, 1)]
+    assert bench.duplicate_devices([dict(a, uuid=None, pci=None), dict(b, uuid=None, pci=None)]) == []

@@ -101,3 +101,19 @@ def test_bench_launcher_two_ranks_share_device():
     assert out["n_gpus"] == 2 and len(out["per_rank_ms_per_step"]) == 2
     assert [tuple(s["frames"]) for s in out["shards"]] == [(0, 3), (2, 5)]
     assert out["value"] > 0
+    assert out["collectives"] == "gloo" and out["distinct_devices"] == 1
+    dev = [s["device"] for s in out["shards"]]
+    assert dev[0]["local"] == dev[1]["local"] == 0 and (dev[0]["uuid"] or dev[0]["pci"])
+
+
+def test_bench_refuses_two_ranks_on_one_gpu():
+    """Without --share-device, two ranks that land on one GPU (forced here) must not report
+    n_gpus = 2: the launch fails, naming the shared device."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--force-device", "0",
+                        "--config", "c2", "--batch", "2", "--steps", "1", "--warmup", "1", "--cpu-seconds", "0",
+                        "--lane-steps", "0", "--launch-timeout", "100"],
+                       capture_output=True, text=True, timeout=150, env=env)
+    assert p.returncode != 0
+    assert "drive the same GPU" in p.stderr
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]

@@ -179,7 +179,7 @@ def test_mixed_frame_and_cuts(ing):
     """A frame of DDC, ADC and DBF records (9 channels and 9 beams pass all three size checks):
     records are located by walking the heads from the first one whose size differs, and cuts
     inside each kind of record stop the frame where the reference stops."""
-    types = [1, 1, 0, 2, 2, 1, 0, 1, 2, 1, 1, 1]
+    types = [1, 1, 0, 2, 3, 2, 1, 0, 1, 2, 255, 1, 1, 1]
     dbf, cfg, stream = synth_mixed_frame(types, 3404, 9, 9, seed=33)
     got, done = _check(ing, stream, dbf, cfg)
     assert done
@@ -188,7 +188,7 @@ def test_mixed_frame_and_cuts(ing):
     offs = [0]
     for t in types:
         offs.append(offs[-1] + 192 + ref.payload_bytes(t, 3404, 9) + 64)
-    for p in (2, 3, 6, 9):   # inside the payload, then inside the tail
+    for p in (2, 3, 4, 7, 10):   # inside the payload, then inside the tail
         _check(ing, stream[:offs[p] + 192 + 1000], dbf, cfg)
         _check(ing, stream[:offs[p + 1] - 10], dbf, cfg)
 
@@ -212,3 +212,28 @@ def test_dbf24_size_error_and_ddc_only(ing):
     _, _, status = ing.decode_dev(d, len(stream), cfg, ing.dbf_device(dbf), ddc_only=True)
     st = status.cpu().numpy()
     assert st[2] == _capi.RSP_PRT_UNSUPPORTED_TYPE and st[4] == 2
+
+
+def test_unknown_type_records_are_zero_rows(ing):
+    """Data types 3..255 (FrameDataRead_xzr.m:110-112 sizes the payload as DBF, :141 only
+    typecasts it, :160-165 has no case): the row stays zeros(point_PRT, beam_num), passes the
+    :171 size check whatever the head's channel and sample counts, and the frame goes on."""
+    import torch
+    from rsp import _capi
+    dbf, cfg, stream = synth_mixed_frame([1, 1, 1], 200, 9, 9, seed=5)
+    rec = len(stream) // 3
+    odd = ref.prt_record(np.zeros((150, 5), np.int8), pulse_no=1, servo=99, pulse_num=4, cfg=cfg, data_type=7,
+                         payload=bytes(range(256)) * 4)
+    stream = stream[:rec] + odd + stream[rec:]
+    cfg = dict(cfg, prtNum=4)
+    want, ang, done, _ = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    assert done and not want[1].any() and ang[1] == 99
+    d = torch.frombuffer(bytearray(stream), dtype=torch.uint8).cuda()
+    out, servo, status = ing.decode_dev(d, len(stream), cfg, ing.dbf_device(dbf))
+    st = status.cpu().numpy()
+    assert (st[:4] == _capi.RSP_PRT_OK).all() and st[4] == 4
+    got = out.cpu().numpy().transpose(1, 2, 0)
+    assert not got[1].any() and int(servo[1].item()) == 99
+    for p in (0, 2, 3):
+        err = np.linalg.norm(got[p] - want[p]) / np.linalg.norm(want[p])
+        assert err < 1e-6, (p, err)

@@ -163,7 +163,7 @@ def test_oracle_dbf24_size_errors(ch):
 def test_oracle_adc_and_mixed_frame():
     """ADC records are the int16 matrix itself (:144-147) and records of different types and
     sizes follow one another (each sized by its own head, :105-119)."""
-    types = [1, 0, 2, 2, 1, 0, 1]
+    types = [1, 0, 2, 3, 2, 1, 0, 200, 1]
     dbf, cfg, stream = synth_mixed_frame(types, 31, 9, 9, seed=4)
     out, ang, done, end = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
     assert done and not end
@@ -175,6 +175,8 @@ def test_oracle_adc_and_mixed_frame():
             np.testing.assert_array_equal(out[p], np.frombuffer(raw[:31 * 9 * 2], "<i2").reshape(31, 9))
         elif t == 2:
             np.testing.assert_array_equal(out[p], _direct_dbf24(raw, 31, 9, 9))
+        elif t > 2:   # no case at :160-165: the zeros(point_PRT, beam_num) row
+            assert not out[p].any()
         off += 192 + size + 64
     assert off == len(stream)
     np.testing.assert_array_equal(ang, 7 * np.arange(len(types)))
@@ -195,9 +197,16 @@ def test_host_reader_stops_where_the_reference_does():
     b = bytearray(stream)
     b[rec0 + 24:rec0 + 28] = (0).to_bytes(4, "little")       # PRT 1: pulse_data_num = 0
     cases["count"] = bytes(b)
+    # a type-7 record whose 5 channels and 12 samples would fail every other type's size check:
+    # no case at :160-165, so the reference keeps a zero row, reads the tail and goes on
+    odd = ref.prt_record(np.zeros((12, 5), np.int8), pulse_no=1, pulse_num=4, cfg=cfg, data_type=7,
+                         payload=bytes(ref.payload_bytes(7, 12, 5)))
+    cases["type7"] = stream[:rec0] + odd + stream[rec0:]
     for name, s in cases.items():
         host, oracle = ingest.BytesStream(s), ref.BytesStream(s)
         data, ended = ingest.Ingest.read_frame_bytes(host, cfg)
         _, _, done, end = ref.FrameReader().read(oracle, dbf, cfg, 0)
         assert host._pos == oracle.pos == len(data), name
         assert ended == end, name
+        if name == "type7":
+            assert done and not end and len(data) == len(s) - rec0   # PRTs 1, 7, 0, 2: the last DDC record unread

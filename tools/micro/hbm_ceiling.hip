@@ -1,11 +1,19 @@
 // Hand-written HBM ceiling on gfx950: streaming copy, read-only and write-only kernels over
-// buffers far larger than the 256 MiB Infinity Cache, at 16 B and 8 B per lane (the chain's
-// row loads are 8 B per lane: one complex fp32 element), over a sweep of workgroups per CU
-// and loads in flight per thread.  The best rate of each kind is the ceiling the chain's
-// counted traffic is compared with (bench.py roofline.ceiling_frac).
+// buffers far larger than the 256 MiB Infinity Cache.  Two kernel forms:
+//
+//  * "oneshot" (round 4, the reported ceiling): every thread moves U 16-B (or 8-B) elements
+//    exactly once -- no grid-stride loop, no per-element guard (the buffer is a whole number
+//    of blocks), 32-bit lane offsets through a per-block buffer resource (the block's base is
+//    in SGPRs; one VGPR offset + immediates per access), all U loads issued before any store.
+//    Optional non-temporal policy (aux 2) on loads and/or stores.
+//  * "stride" (round 3's form, kept for comparison): a grid-stride loop with 64-bit indices and
+//    a guard per element, at 2..32 workgroups per CU.
+//
+// The best copy rate is the ceiling the chain's counted traffic is compared with
+// (bench.py roofline.ceiling_frac).
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/micro/hbm_ceiling.hip -o tools/micro/hbm_ceiling
-//   tools/micro/hbm_ceiling [GiB per buffer, default 2] > profiles/r03/hbm_ceiling.txt
+//   tools/micro/hbm_ceiling [GiB per buffer, default 2] > profiles/r04/hbm_ceiling.txt
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -19,17 +27,77 @@
         }                                                                                  \
     } while (0)
 
-// KIND 0: copy (read src, write dst); 1: read-only (sum, stored only on an impossible value);
-// 2: write-only (fill).  T = float4 (16 B/lane) or float2 (8 B/lane).  U elements per thread
-// per iteration, all loads issued before any use.
-template <typename T> __device__ __forceinline__ float first(T v) { return v.x; }
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+template <int W> struct Vec;
+template <> struct Vec<16> {
+    typedef v4i T;
+    static __device__ __forceinline__ T ld(__amdgpu_buffer_rsrc_t r, uint32_t v, int aux) {
+        return aux ? __builtin_amdgcn_raw_buffer_load_b128(r, v, 0, 2) : __builtin_amdgcn_raw_buffer_load_b128(r, v, 0, 0);
+    }
+    static __device__ __forceinline__ void st(T x, __amdgpu_buffer_rsrc_t r, uint32_t v, int aux) {
+        if (aux) __builtin_amdgcn_raw_buffer_store_b128(x, r, v, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(x, r, v, 0, 0);
+    }
+    static __device__ __forceinline__ int first(T x) { return x.x; }
+    static __device__ __forceinline__ T fill(uint32_t i) { return T{(int)i, (int)i, (int)i, (int)i}; }
+};
+template <> struct Vec<8> {
+    typedef v2i T;
+    static __device__ __forceinline__ T ld(__amdgpu_buffer_rsrc_t r, uint32_t v, int aux) {
+        return aux ? __builtin_amdgcn_raw_buffer_load_b64(r, v, 0, 2) : __builtin_amdgcn_raw_buffer_load_b64(r, v, 0, 0);
+    }
+    static __device__ __forceinline__ void st(T x, __amdgpu_buffer_rsrc_t r, uint32_t v, int aux) {
+        if (aux) __builtin_amdgcn_raw_buffer_store_b64(x, r, v, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b64(x, r, v, 0, 0);
+    }
+    static __device__ __forceinline__ int first(T x) { return x.x; }
+    static __device__ __forceinline__ T fill(uint32_t i) { return T{(int)i, (int)i}; }
+};
+
+// KIND 0 copy, 1 read-only, 2 write-only.  Block b owns bytes [b*CH, (b+1)*CH), CH = 256*U*W.
+// LNT / SNT: non-temporal loads / stores (compile-time, so each variant is one clean stream).
+template <int KIND, int W, int U, int LNT, int SNT>
+__global__ __launch_bounds__(256) void oneshot(const char* __restrict__ src, char* __restrict__ dst,
+                                               int* __restrict__ sink) {
+    using V = Vec<W>;
+    constexpr uint32_t CH = 256u * U * W;
+    const size_t off = (size_t)blockIdx.x * CH;
+    const auto rs = rsrc(src + off, CH);
+    const auto rd = rsrc(dst + off, CH);
+    const uint32_t v0 = threadIdx.x * W;
+    typename V::T x[U];
+    if constexpr (KIND != 2) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = V::ld(rs, v0 + u * 256u * W, LNT);
+    }
+    if constexpr (KIND == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) V::st(x[u], rd, v0 + u * 256u * W, SNT);
+    } else if constexpr (KIND == 1) {
+        int acc = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= V::first(x[u]);
+        if (acc == 0x5a5a5a5a) sink[threadIdx.x] = acc;
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) V::st(V::fill(blockIdx.x ^ u), rd, v0 + u * 256u * W, SNT);
+    }
+}
+
+// round 3's grid-stride form (64-bit index, a guard per element)
+template <typename T> __device__ __forceinline__ float first(T v) { return v.x; }
 template <int KIND, typename T, int U>
-__global__ __launch_bounds__(256) void stream(const T* __restrict__ src, T* __restrict__ dst, size_t n,
+__global__ __launch_bounds__(256) void stride(const T* __restrict__ src, T* __restrict__ dst, size_t n,
                                               float* __restrict__ sink) {
-    const size_t stride = (size_t)gridDim.x * 256 * U;
+    const size_t step = (size_t)gridDim.x * 256 * U;
     float acc = 0.f;
-    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < n; base += stride) {
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < n; base += step) {
         T v[U];
         if constexpr (KIND != 2) {
 #pragma unroll
@@ -56,76 +124,119 @@ __global__ __launch_bounds__(256) void stream(const T* __restrict__ src, T* __re
     if (KIND == 1 && acc == 1234567.f) sink[threadIdx.x] = acc;
 }
 
-template <int KIND, typename T, int U>
-static double run(const void* src, void* dst, size_t bytes, float* sink, int grid, int reps) {
-    const size_t n = bytes / sizeof(T);
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0));
-    CK(hipEventCreate(&e1));
-    hipLaunchKernelGGL((stream<KIND, T, U>), dim3(grid), dim3(256), 0, 0, (const T*)src, (T*)dst, n, sink);
+static hipEvent_t g_e0, g_e1;
+
+template <typename F>
+static double best_ms(F launch, int reps) {
+    launch();
     CK(hipDeviceSynchronize());
     float best = 1e30f;
     for (int r = 0; r < reps; ++r) {
-        CK(hipEventRecord(e0));
-        hipLaunchKernelGGL((stream<KIND, T, U>), dim3(grid), dim3(256), 0, 0, (const T*)src, (T*)dst, n, sink);
-        CK(hipEventRecord(e1));
-        CK(hipEventSynchronize(e1));
+        CK(hipEventRecord(g_e0));
+        launch();
+        CK(hipEventRecord(g_e1));
+        CK(hipEventSynchronize(g_e1));
         float ms = 0.f;
-        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipEventElapsedTime(&ms, g_e0, g_e1));
         if (ms < best) best = ms;
     }
-    CK(hipEventDestroy(e0));
-    CK(hipEventDestroy(e1));
-    const double moved = (KIND == 0 ? 2.0 : 1.0) * (double)n * sizeof(T);
-    return moved / (best * 1e-3) / 1e9;   // GB/s
+    return best;
+}
+
+template <int KIND, int W, int U, int LNT, int SNT>
+static double run_oneshot(const char* name, const void* src, void* dst, size_t bytes, int* sink) {
+    constexpr size_t CH = 256u * U * W;
+    const unsigned grid = (unsigned)(bytes / CH);
+    const double ms = best_ms([&] {
+        hipLaunchKernelGGL((oneshot<KIND, W, U, LNT, SNT>), dim3(grid), dim3(256), 0, 0, (const char*)src, (char*)dst,
+                           sink);
+    }, 7);
+    const double moved = (KIND == 0 ? 2.0 : 1.0) * (double)grid * CH;
+    const double g = moved / (ms * 1e-3) / 1e9;
+    printf("  oneshot %-5s %2dB/lane U=%-2d ld_nt=%d st_nt=%d  %7u blocks  %8.1f GB/s\n", name, W, U, LNT, SNT, grid, g);
+    fflush(stdout);
+    return g;
 }
 
 template <int KIND, typename T, int U>
-static double sweep(const char* name, const void* src, void* dst, size_t bytes, float* sink, int cus) {
+static double run_stride(const char* name, const void* src, void* dst, size_t bytes, float* sink, int cus) {
+    const size_t n = bytes / sizeof(T);
     double best = 0.0;
     int best_wg = 0;
-    for (int wg : {2, 4, 8, 16, 32}) {
-        const double g = run<KIND, T, U>(src, dst, bytes, sink, wg * cus, 5);
-        printf("  %-8s %2dB/lane U=%d  %2d WG/CU  %8.1f GB/s\n", name, (int)sizeof(T), U, wg, g);
+    for (int wg : {4, 8, 16, 32}) {
+        const double ms = best_ms([&] {
+            hipLaunchKernelGGL((stride<KIND, T, U>), dim3(wg * cus), dim3(256), 0, 0, (const T*)src, (T*)dst, n, sink);
+        }, 5);
+        const double g = (KIND == 0 ? 2.0 : 1.0) * (double)n * sizeof(T) / (ms * 1e-3) / 1e9;
         if (g > best) {
             best = g;
             best_wg = wg;
         }
     }
-    printf("BEST %-8s %2dB/lane U=%d  %8.1f GB/s (%d WG/CU)\n", name, (int)sizeof(T), U, best, best_wg);
+    printf("  stride  %-5s %2dB/lane U=%d  best %8.1f GB/s (%d WG/CU)\n", name, (int)sizeof(T), U, best, best_wg);
     fflush(stdout);
     return best;
 }
 
+static double mx(std::initializer_list<double> v) {
+    double m = 0;
+    for (double x : v) m = x > m ? x : m;
+    return m;
+}
+
 int main(int argc, char** argv) {
     const double gib = argc > 1 ? atof(argv[1]) : 2.0;
-    const size_t bytes = (size_t)(gib * (1ull << 30));
+    const size_t bytes = ((size_t)(gib * (1ull << 30)) >> 20) << 20;
     int dev = 0, cus = 0;
     CK(hipGetDevice(&dev));
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    CK(hipEventCreate(&g_e0));
+    CK(hipEventCreate(&g_e1));
     void *src, *dst;
-    float* sink;
+    float* fsink;
+    int* sink;
     CK(hipMalloc(&src, bytes));
     CK(hipMalloc(&dst, bytes));
-    CK(hipMalloc(&sink, 256 * sizeof(float)));
-    CK(hipMemset(src, 0, bytes));
+    CK(hipMalloc(&fsink, 256 * sizeof(float)));
+    CK(hipMalloc(&sink, 256 * sizeof(int)));
+    CK(hipMemset(src, 1, bytes));
     CK(hipMemset(dst, 0, bytes));
-    printf("hbm_ceiling: %.2f GiB per buffer, %d CUs, best of 5 launches per point\n", gib, cus);
-    double c16 = 0, r16 = 0, w16 = 0, c8 = 0, r8 = 0, w8 = 0;
-    for (int pass = 0; pass < 2; ++pass) {   // two passes: the second is the reported one
-        if (pass == 1) printf("-- pass 2 (reported)\n");
-        c16 = sweep<0, float4, 4>("copy", src, dst, bytes, sink, cus);
-        r16 = sweep<1, float4, 4>("read", src, dst, bytes, sink, cus);
-        w16 = sweep<2, float4, 4>("write", src, dst, bytes, sink, cus);
-        c8 = sweep<0, float2, 8>("copy", src, dst, bytes, sink, cus);
-        r8 = sweep<1, float2, 8>("read", src, dst, bytes, sink, cus);
-        w8 = sweep<2, float2, 8>("write", src, dst, bytes, sink, cus);
+    printf("hbm_ceiling: %.2f GiB per buffer, %d CUs, best of 7 launches per point (5 for stride)\n",
+           (double)bytes / (1 << 30), cus);
+    double copy = 0, read = 0, write = 0, copy8 = 0, copy_stride = 0, read_stride = 0, write_stride = 0;
+    for (int pass = 0; pass < 2; ++pass) {   // the second pass is the reported one
+        printf("-- pass %d%s\n", pass + 1, pass ? " (reported)" : "");
+        copy = mx({run_oneshot<0, 16, 4, 0, 0>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 8, 0, 0>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 16, 0, 0>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 4, 1, 0>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 4, 0, 1>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 4, 1, 1>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 8, 1, 1>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 2, 0, 0>("copy", src, dst, bytes, sink),
+                   run_oneshot<0, 16, 1, 0, 0>("copy", src, dst, bytes, sink)});
+        copy8 = mx({run_oneshot<0, 8, 8, 0, 0>("copy", src, dst, bytes, sink),
+                    run_oneshot<0, 8, 16, 0, 0>("copy", src, dst, bytes, sink),
+                    run_oneshot<0, 8, 8, 1, 1>("copy", src, dst, bytes, sink)});
+        read = mx({run_oneshot<1, 16, 4, 0, 0>("read", src, dst, bytes, sink),
+                   run_oneshot<1, 16, 8, 0, 0>("read", src, dst, bytes, sink),
+                   run_oneshot<1, 16, 16, 0, 0>("read", src, dst, bytes, sink),
+                   run_oneshot<1, 16, 4, 1, 0>("read", src, dst, bytes, sink)});
+        write = mx({run_oneshot<2, 16, 4, 0, 0>("write", src, dst, bytes, sink),
+                    run_oneshot<2, 16, 8, 0, 0>("write", src, dst, bytes, sink),
+                    run_oneshot<2, 16, 1, 0, 0>("write", src, dst, bytes, sink),
+                    run_oneshot<2, 16, 4, 0, 1>("write", src, dst, bytes, sink)});
+        copy_stride = run_stride<0, float4, 4>("copy", src, dst, bytes, fsink, cus);
+        read_stride = run_stride<1, float4, 4>("read", src, dst, bytes, fsink, cus);
+        write_stride = run_stride<2, float4, 4>("write", src, dst, bytes, fsink, cus);
     }
-    printf("{\"copy_16B_GBps\": %.1f, \"read_16B_GBps\": %.1f, \"write_16B_GBps\": %.1f, "
-           "\"copy_8B_GBps\": %.1f, \"read_8B_GBps\": %.1f, \"write_8B_GBps\": %.1f, \"bytes_per_buffer\": %zu}\n",
-           c16, r16, w16, c8, r8, w8, bytes);
+    printf("{\"copy_GBps\": %.1f, \"read_GBps\": %.1f, \"write_GBps\": %.1f, \"copy_8B_GBps\": %.1f, "
+           "\"copy_stride_GBps\": %.1f, \"read_stride_GBps\": %.1f, \"write_stride_GBps\": %.1f, "
+           "\"bytes_per_buffer\": %zu}\n",
+           copy, read, write, copy8, copy_stride, read_stride, write_stride, bytes);
     CK(hipFree(src));
     CK(hipFree(dst));
+    CK(hipFree(fsink));
     CK(hipFree(sink));
     return 0;
 }
