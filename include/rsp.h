@@ -49,7 +49,8 @@
 extern "C" {
 #endif
 
-#define RSP_ABI_VERSION 2   /* 2: rsp_set_fused / rsp_chain_check removed, rsp_set_pc_split added */
+#define RSP_ABI_VERSION 3   /* 2: rsp_set_fused / rsp_chain_check removed, rsp_set_pc_split added;
+                               3: rsp_set_host_pipeline */
 #define RSP_MAX_SEG 4
 #define RSP_MAX_FIR_TAPS 64
 
@@ -187,6 +188,15 @@ int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 int rsp_set_streams(rsp_ctx* ctx, int32_t n);
 
 /* ---- host-buffer entry points (MEX / fun_MTD_produce drop-in), synchronous ---------- */
+/* rsp_pc_mtd_cfar / rsp_pc_mtd take pageable host buffers (MATLAB's arrays) and pipeline the
+ * call in chunks of CPIs: chunk k's host->device copy, chain and device->host copy overlap
+ * chunks k+1 and k-1 (two copy streams beside the context's stream); the pageable <-> pinned
+ * staging runs through rings of 8 MiB pinned pieces copied by a host thread pool, so the copies
+ * of one CPI also overlap their DMA.  Outputs are identical to the _dev path's. */
+/* CPIs per host chunk (0 = by size: 32 MiB of input) and host copy threads (0 = default:
+ * 8 with >= 16 hardware threads). */
+int rsp_set_host_pipeline(rsp_ctx* ctx, int64_t cpis_per_chunk, int32_t copy_threads);
+
 int rsp_pc_mtd(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,
                int64_t P, int64_t R, int64_t batch, float* rdm_out, int32_t rdm_layout);
 

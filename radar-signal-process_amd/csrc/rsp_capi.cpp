@@ -15,10 +15,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rsp.h"
+#include "rsp_hostpool.h"
 #include "rsp_internal.h"
 
 using cd = std::complex<double>;
@@ -60,7 +63,25 @@ struct rsp_ctx {
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
     DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
     DevBuf ing_meta;                    // ingest: per-PRT record offsets and types
-    DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging
+    DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging (rsp_cfar)
+    // Pipelined host-buffer path (rsp_pc_mtd_cfar / rsp_pc_mtd): chunk k's H2D (copy stream),
+    // chain (ctx->stream) and D2H (copy stream) overlap chunks k+1 and k-1; pageable <-> pinned
+    // staging through rings of pinned pieces, copied by a host thread pool.
+    struct HostPipe {
+        static constexpr int kSlots = 2;      // chunk slots (device buffers)
+        static constexpr int kRing = 4;       // pinned pieces per direction
+        hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+        DevBuf in[kSlots], canon[kSlots], rdm[kSlots], flag[kSlots], flagV[kSlots], tr[kSlots][3];
+        hipEvent_t ev_in[kSlots] = {}, ev_comp[kSlots] = {}, ev_out[kSlots] = {};
+        void* pin_in[kRing] = {};
+        void* pin_out[kRing] = {};
+        hipEvent_t ev_pin_in[kRing] = {}, ev_pin_out[kRing] = {};
+        size_t piece = 0;                     // bytes per pinned piece
+        int ring_in = 0;                      // next input piece slot
+        int threads = 0;                      // requested copy threads (0 = default)
+        std::unique_ptr<rsp::CopyPool> pool;
+    } hp;
+    int64_t host_chunk = 0;                   // CPIs per host chunk (0 = by bytes)
     // diagnostics (rsp_profile): HIP event pairs around each kernel launch
     struct Ev {
         int k;
@@ -255,7 +276,7 @@ static void zero_v_band(int64_t rows, int div, int* lo, int* hi) {
 }
 
 // ------------------------------------------------------------------ public API
-const char* rsp_version(void) { return "rsp-mi355x 0.3.0 (gfx950, abi 2)"; }
+const char* rsp_version(void) { return "rsp-mi355x 0.4.0 (gfx950, abi 3)"; }
 
 const char* rsp_last_error(const rsp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
@@ -275,6 +296,27 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (int i = 0; i < 3; ++i) {
         if (ctx->aux[i]) hipStreamDestroy(ctx->aux[i]);
         if (ctx->ev_join[i]) hipEventDestroy(ctx->ev_join[i]);
+    }
+    {
+        auto& h = ctx->hp;
+        for (int i = 0; i < h.kSlots; ++i) {
+            DevBuf* hb[] = {&h.in[i], &h.canon[i], &h.rdm[i], &h.flag[i], &h.flagV[i], &h.tr[i][0], &h.tr[i][1],
+                            &h.tr[i][2]};
+            for (DevBuf* b : hb)
+                if (b->p) hipFree(b->p);
+            if (h.ev_in[i]) hipEventDestroy(h.ev_in[i]);
+            if (h.ev_comp[i]) hipEventDestroy(h.ev_comp[i]);
+            if (h.ev_out[i]) hipEventDestroy(h.ev_out[i]);
+        }
+        for (int i = 0; i < h.kRing; ++i) {
+            if (h.pin_in[i]) hipHostFree(h.pin_in[i]);
+            if (h.pin_out[i]) hipHostFree(h.pin_out[i]);
+            if (h.ev_pin_in[i]) hipEventDestroy(h.ev_pin_in[i]);
+            if (h.ev_pin_out[i]) hipEventDestroy(h.ev_pin_out[i]);
+        }
+        if (h.s_h2d) hipStreamDestroy(h.s_h2d);
+        if (h.s_d2h) hipStreamDestroy(h.s_d2h);
+        h.pool.reset();
     }
     if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_scratch) hipEventDestroy(ctx->ev_scratch);
@@ -1305,29 +1347,6 @@ static size_t dtype_size(int32_t dtype) {
     }
 }
 
-// H2D + conversion into the canonical device layout; returns the device echo pointer.
-static int stage_echo(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t batch,
-                      const void** d_echo, int32_t* d_dtype) {
-    const int64_t P = ctx->p.P, R = ctx->p.R;
-    const size_t esz = dtype_size(dtype);
-    const size_t bytes = (size_t)batch * P * R * esz;
-    int rc = ensure(ctx, ctx->st_in, bytes);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->st_in.p, echo, bytes, hipMemcpyHostToDevice, ctx->stream));
-    if (layout == RSP_ROWMAJOR && (dtype == RSP_C64 || dtype == RSP_C32F16)) {
-        *d_echo = ctx->st_in.p;
-        *d_dtype = dtype;
-        return RSP_OK;
-    }
-    rc = ensure(ctx, ctx->st_canon, (size_t)batch * P * R * sizeof(float2));
-    if (rc) return rc;
-    HIP_TRY(ctx, rsp::launch_ingest(ctx->st_in.p, dtype, layout, (float2*)ctx->st_canon.p, batch, (int)P,
-                                    (int)R, ctx->stream));
-    *d_echo = ctx->st_canon.p;
-    *d_dtype = RSP_C64;
-    return RSP_OK;
-}
-
 template <typename T>
 static int fetch(rsp_ctx* ctx, const T* d, T* h, int64_t batch, int64_t A, int64_t B, int32_t layout) {
     const size_t n = (size_t)batch * A * B;
@@ -1360,6 +1379,106 @@ static int check_host_call(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_
     return RSP_OK;
 }
 
+// ---- pipelined host path
+static constexpr size_t kHostPiece = 8u << 20;        // pinned piece
+static constexpr size_t kHostChunkBytes = 32u << 20;  // input bytes per host chunk
+
+static int host_pipe_init(rsp_ctx* ctx) {
+    auto& h = ctx->hp;
+    if (h.s_h2d) return RSP_OK;
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&h.s_h2d, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&h.s_d2h, hipStreamNonBlocking));
+    for (int i = 0; i < h.kSlots; ++i) {
+        HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_in[i], hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_comp[i], hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_out[i], hipEventDisableTiming));
+    }
+    h.piece = kHostPiece;
+    for (int i = 0; i < h.kRing; ++i) {
+        HIP_TRY(ctx, hipHostMalloc(&h.pin_in[i], h.piece, hipHostMallocDefault));
+        HIP_TRY(ctx, hipHostMalloc(&h.pin_out[i], h.piece, hipHostMallocDefault));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_pin_in[i], hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_pin_out[i], hipEventDisableTiming));
+    }
+    return RSP_OK;
+}
+
+static rsp::CopyPool& host_pool(rsp_ctx* ctx) {
+    auto& h = ctx->hp;
+    int want = h.threads;
+    if (want <= 0) {
+        const unsigned hc = std::thread::hardware_concurrency();
+        want = hc >= 16 ? 8 : (hc >= 4 ? (int)hc / 2 : 1);
+    }
+    if (!h.pool || h.pool->threads() != want) h.pool.reset(new rsp::CopyPool(want));
+    return *h.pool;
+}
+
+// host (pageable) -> device, through the pinned input ring on the H2D stream: piece i is
+// copied into a ring slot by the pool while the DMA of piece i-1 runs.
+static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes) {
+    auto& h = ctx->hp;
+    rsp::CopyPool& pool = host_pool(ctx);
+    for (size_t off = 0; off < bytes; off += h.piece) {
+        const size_t n = bytes - off < h.piece ? bytes - off : h.piece;
+        const int r = h.ring_in;
+        h.ring_in = (h.ring_in + 1) % h.kRing;
+        HIP_TRY(ctx, hipEventSynchronize(h.ev_pin_in[r]));   // the slot's previous DMA is done
+        pool.copy(h.pin_in[r], (const char*)src + off, n);
+        HIP_TRY(ctx, hipMemcpyAsync((char*)d + off, h.pin_in[r], n, hipMemcpyHostToDevice, h.s_h2d));
+        HIP_TRY(ctx, hipEventRecord(h.ev_pin_in[r], h.s_h2d));
+    }
+    return RSP_OK;
+}
+
+// device -> host (pageable), through the pinned output ring on the D2H stream: up to kRing
+// pieces in flight; each is copied out by the pool once its DMA is done.
+struct D2HPart {
+    const void* d;
+    void* h;
+    size_t bytes;
+};
+static int d2h_pieces(rsp_ctx* ctx, const std::vector<D2HPart>& parts) {
+    auto& h = ctx->hp;
+    rsp::CopyPool& pool = host_pool(ctx);
+    struct Piece {
+        const char* d;
+        char* h;
+        size_t n;
+    };
+    std::vector<Piece> ps;
+    for (const D2HPart& p : parts)
+        for (size_t off = 0; off < p.bytes; off += h.piece)
+            ps.push_back({(const char*)p.d + off, (char*)p.h + off, p.bytes - off < h.piece ? p.bytes - off : h.piece});
+    const size_t np = ps.size();
+    auto issue = [&](size_t i) -> int {
+        const int r = (int)(i % h.kRing);
+        HIP_TRY(ctx, hipMemcpyAsync(h.pin_out[r], ps[i].d, ps[i].n, hipMemcpyDeviceToHost, h.s_d2h));
+        HIP_TRY(ctx, hipEventRecord(h.ev_pin_out[r], h.s_d2h));
+        return RSP_OK;
+    };
+    int rc;
+    for (size_t i = 0; i < np && i < (size_t)h.kRing; ++i)
+        if ((rc = issue(i))) return rc;
+    for (size_t i = 0; i < np; ++i) {
+        const int r = (int)(i % h.kRing);
+        HIP_TRY(ctx, hipEventSynchronize(h.ev_pin_out[r]));
+        pool.copy(ps[i].h, h.pin_out[r], ps[i].n);
+        if (i + h.kRing < np && (rc = issue(i + h.kRing))) return rc;
+    }
+    return RSP_OK;
+}
+
+int rsp_set_host_pipeline(rsp_ctx* ctx, int64_t cpis_per_chunk, int32_t copy_threads) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "null ctx");
+    if (cpis_per_chunk < 0 || copy_threads < 0 || copy_threads > 64)
+        return fail(ctx, RSP_ERR_ARG, "rsp_set_host_pipeline: chunk %lld, threads %d", (long long)cpis_per_chunk,
+                    (int)copy_threads);
+    ctx->host_chunk = cpis_per_chunk;
+    ctx->hp.threads = copy_threads;
+    return RSP_OK;
+}
+
 int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
                     int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
                     uint8_t* flag_out, uint8_t* flagV_out) {
@@ -1370,28 +1489,88 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
     if (cfar && !flag_out) return fail(ctx, RSP_ERR_ARG, "CFAR requested without flag_out");
     if (!cfar && !rdm_out) return fail(ctx, RSP_ERR_ARG, "no output requested");
     if (batch == 0) return RSP_OK;
-    const void* d_echo = nullptr;
-    int32_t d_dtype = RSP_C64;
-    rc = stage_echo(ctx, echo, dtype, layout, batch * ctx->beams, &d_echo, &d_dtype);   // [batch][beams][P][R]
-    if (rc) return rc;
-    const int64_t Ro = ctx->p.R_out, V = ctx->V;
-    const size_t cells = (size_t)batch * V * Ro;
-    if ((rc = ensure(ctx, ctx->st_rdm, cells * sizeof(float)))) return rc;
-    if (cfar) {
-        if ((rc = ensure(ctx, ctx->st_flag, cells))) return rc;
-        if ((rc = ensure(ctx, ctx->st_flagV, cells))) return rc;
+    if ((rc = host_pipe_init(ctx))) return rc;
+    auto& h = ctx->hp;
+    const int64_t Ro = ctx->p.R_out, V = ctx->V, beams = ctx->beams;
+    const size_t in_cpi = (size_t)beams * P * R * dtype_size(dtype);
+    const size_t cells = (size_t)V * Ro;   // per CPI
+    const bool conv = !(layout == RSP_ROWMAJOR && (dtype == RSP_C64 || dtype == RSP_C32F16));
+    const bool tr = out_layout == RSP_COLMAJOR;
+    const bool want_fv = cfar && flagV_out;
+    int64_t K = ctx->host_chunk > 0 ? ctx->host_chunk : (int64_t)(kHostChunkBytes / in_cpi);
+    if (K < 1) K = 1;
+    if (K > batch) K = batch;
+    const int64_t nk = (batch + K - 1) / K;
+    for (int i = 0; i < h.kSlots && i < nk; ++i) {
+        if ((rc = ensure(ctx, h.in[i], (size_t)K * in_cpi))) return rc;
+        if (conv && (rc = ensure(ctx, h.canon[i], (size_t)K * beams * P * R * sizeof(float2)))) return rc;
+        if ((rc = ensure(ctx, h.rdm[i], (size_t)K * cells * sizeof(float)))) return rc;
+        if (cfar && (rc = ensure(ctx, h.flag[i], (size_t)K * cells))) return rc;
+        if (want_fv && (rc = ensure(ctx, h.flagV[i], (size_t)K * cells))) return rc;
+        if (tr) {
+            if (rdm_out && (rc = ensure(ctx, h.tr[i][0], (size_t)K * cells * sizeof(float)))) return rc;
+            if (cfar && (rc = ensure(ctx, h.tr[i][1], (size_t)K * cells))) return rc;
+            if (want_fv && (rc = ensure(ctx, h.tr[i][2], (size_t)K * cells))) return rc;
+        }
     }
-    rc = rsp_pc_mtd_cfar_dev(ctx, d_echo, d_dtype, batch, cfar, (float*)ctx->st_rdm.p,
-                             cfar ? (uint8_t*)ctx->st_flag.p : nullptr, cfar ? (uint8_t*)ctx->st_flagV.p : nullptr,
-                             ctx->stream);
-    if (rc) return rc;
-    if (rdm_out && (rc = fetch(ctx, (const float*)ctx->st_rdm.p, rdm_out, batch, V, Ro, out_layout))) return rc;
-    if (cfar) {
-        if ((rc = fetch(ctx, (const uint8_t*)ctx->st_flag.p, flag_out, batch, V, Ro, out_layout))) return rc;
-        if (flagV_out &&
-            (rc = fetch(ctx, (const uint8_t*)ctx->st_flagV.p, flagV_out, batch, V, Ro, out_layout)))
+    // chunk k: the chain on slot k % 2 after its H2D, then transposes; its outputs' D2H waits for it
+    auto chunk_n = [&](int64_t k) { return k == nk - 1 ? batch - k * K : K; };
+    auto compute = [&](int64_t k) -> int {
+        const int sl = (int)(k % h.kSlots);
+        const int64_t n = chunk_n(k);
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_in[sl], 0));
+        if (k >= h.kSlots) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_out[sl], 0));   // slot's D2H done
+        const void* d_echo = h.in[sl].p;
+        int32_t d_dtype = dtype;
+        if (conv) {
+            HIP_TRY(ctx, rsp::launch_ingest(h.in[sl].p, dtype, layout, (float2*)h.canon[sl].p, n * beams, (int)P,
+                                            (int)R, ctx->stream));
+            d_echo = h.canon[sl].p;
+            d_dtype = RSP_C64;
+        }
+        int rc2 = rsp_pc_mtd_cfar_dev(ctx, d_echo, d_dtype, n, cfar, (float*)h.rdm[sl].p,
+                                      cfar ? (uint8_t*)h.flag[sl].p : nullptr,
+                                      want_fv ? (uint8_t*)h.flagV[sl].p : nullptr, ctx->stream);
+        if (rc2) return rc2;
+        if (tr) {
+            if (rdm_out)
+                HIP_TRY(ctx, rsp::launch_transpose_f32((const float*)h.rdm[sl].p, (float*)h.tr[sl][0].p, n, (int)V,
+                                                       (int)Ro, ctx->stream));
+            if (cfar)
+                HIP_TRY(ctx, rsp::launch_transpose_u8((const uint8_t*)h.flag[sl].p, (uint8_t*)h.tr[sl][1].p, n, (int)V,
+                                                      (int)Ro, ctx->stream));
+            if (want_fv)
+                HIP_TRY(ctx, rsp::launch_transpose_u8((const uint8_t*)h.flagV[sl].p, (uint8_t*)h.tr[sl][2].p, n,
+                                                      (int)V, (int)Ro, ctx->stream));
+        }
+        HIP_TRY(ctx, hipEventRecord(h.ev_comp[sl], ctx->stream));
+        return RSP_OK;
+    };
+    auto output = [&](int64_t k) -> int {
+        const int sl = (int)(k % h.kSlots);
+        const size_t n = (size_t)chunk_n(k), o = (size_t)k * K * cells;
+        HIP_TRY(ctx, hipStreamWaitEvent(h.s_d2h, h.ev_comp[sl], 0));
+        std::vector<D2HPart> parts;
+        if (rdm_out) parts.push_back({tr ? h.tr[sl][0].p : h.rdm[sl].p, rdm_out + o, n * cells * sizeof(float)});
+        if (cfar) parts.push_back({tr ? h.tr[sl][1].p : h.flag[sl].p, flag_out + o, n * cells});
+        if (want_fv) parts.push_back({tr ? h.tr[sl][2].p : h.flagV[sl].p, flagV_out + o, n * cells});
+        int rc2 = d2h_pieces(ctx, parts);
+        if (rc2) return rc2;
+        HIP_TRY(ctx, hipEventRecord(h.ev_out[sl], h.s_d2h));
+        return RSP_OK;
+    };
+    for (int64_t k = 0; k < nk; ++k) {
+        const int sl = (int)(k % h.kSlots);
+        // the slot's previous chain (chunk k-2) has read its input
+        if (k >= h.kSlots) HIP_TRY(ctx, hipStreamWaitEvent(h.s_h2d, h.ev_comp[sl], 0));
+        if ((rc = h2d_pieces(ctx, h.in[sl].p, (const char*)echo + (size_t)k * K * in_cpi, (size_t)chunk_n(k) * in_cpi)))
             return rc;
+        HIP_TRY(ctx, hipEventRecord(h.ev_in[sl], h.s_h2d));
+        if ((rc = compute(k))) return rc;
+        if (k >= 1 && (rc = output(k - 1))) return rc;
     }
+    if ((rc = output(nk - 1))) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(h.s_d2h));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return RSP_OK;
 }

@@ -296,6 +296,56 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
     xsync<WS>();
 }
 
+// Row input by LDS-DMA (dev-only -DRSP_PC_DMA, A/B of VERDICT r3 item 1): a long row's N input
+// samples go global -> its LDS exchange slot by `buffer_load_dwordx4 ... lds` (16 B per lane, 1 KiB
+// contiguous per wave instruction, no VGPR destination), then each thread reads its strided
+// elements u[m] = x[t + G*m] from the slot (lane-contiguous ds_read_b64: conflict-free).  The
+// buffer range check supplies the zero padding past in_len; the 16-byte access that straddles
+// in_len is dropped whole by the rsrc (num_records rounded down to 16 B) and its in-range
+// elements re-read by the lane that owns it before the barrier.
+template <int N, int G, typename TIn>
+__host__ __device__ constexpr bool kDmaIn() {
+#ifdef RSP_PC_DMA
+    return G >= 256 && G % 64 == 0 && (N * (int)sizeof(TIn)) % (G * 16) == 0;
+#else
+    return false;
+#endif
+}
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename TIn, int N, int G>
+__device__ __forceinline__ void pc_dma_issue(const TIn* x, uint32_t nbytes, float2* slot, int t) {
+    constexpr int NQ = N * (int)sizeof(TIn) / (G * 16);
+    const auto xr = buf_rsrc(x, nbytes & ~15u);
+    const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
+    char* l = reinterpret_cast<char*>(slot);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(l + (q * G + wb) * 16), 16, (uint32_t)(q * G + t) * 16u,
+                                                  0, 0, 0);
+}
+
+template <typename TIn, int N, int G>
+__device__ __forceinline__ void pc_dma_read(float2 (&u)[N / G], const TIn* x, uint32_t nbytes, float2* slot, int t) {
+    constexpr int E = N / G;
+    constexpr uint32_t ES = sizeof(TIn);
+    // the straddling 16 bytes [nb16, nb16 + 16) hold (nbytes - nb16) / ES in-range elements
+    const uint32_t nb16 = nbytes & ~15u;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nb16 < nbytes && (uint32_t)(nb16 / 16u) % G == (uint32_t)t) {
+        const auto xr = buf_rsrc(x, nbytes);
+        TIn* l = reinterpret_cast<TIn*>(slot);
+        for (uint32_t o = nb16; o < nbytes; o += ES) {
+            if constexpr (ES == 8) l[o / ES] = buf_ld_f2(xr, o, 0u);
+            else l[o / ES] = __builtin_bit_cast(TIn, __builtin_amdgcn_raw_buffer_load_b32(xr, o, 0u, 0));
+        }
+    }
+    __syncthreads();
+    const TIn* l = reinterpret_cast<const TIn*>(slot);
+#pragma unroll
+    for (int m = 0; m < E; ++m) u[m] = ld_c(l + t + G * m);
+}
+
 // One row's matched-filter segment (and optionally its FIR segment) by G threads.
 // G >= 64: a row spans whole waves, so the row index is wave-uniform (readfirstlane makes
 // that visible to the compiler) and the row's input/output spans are buffer resources in
@@ -353,7 +403,9 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     constexpr int NW = tw_regs<N, E>() > 0 ? tw_regs<N, E>() : 1;
     float2 w[NW];
     tw_preload<N, G, 1, E, 0, NW>(w, t, tw);
-    if constexpr (kUniform) {
+    if constexpr (kDmaIn<N, G, TIn>()) {
+        pc_dma_issue<TIn, N, G>(x + in_start, valid ? (uint32_t)in_len * ES : 0u, buf, t);
+    } else if constexpr (kUniform) {
         const auto xr = buf_rsrc(x + in_start, valid ? (uint32_t)in_len * ES : 0u);
 #pragma unroll
         for (int m = 0; m < E; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)e0 * ES, (uint32_t)(G * m) * ES);
@@ -364,15 +416,22 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             u[m] = (valid && i < in_len) ? ld_c(x + in_start + i) : make_float2(0.f, 0.f);
         }
     }
-    if (a.gain) {   // fused iSTC (rsp_set_prefilter): echo column n times gain[n]
-        const auto gr = buf_rsrc(a.gain + in_start, (uint32_t)in_len * 4u);
+    auto apply_gain = [&] {
+        if (a.gain) {   // fused iSTC (rsp_set_prefilter): echo column n times gain[n]
+            const auto gr = buf_rsrc(a.gain + in_start, (uint32_t)in_len * 4u);
 #pragma unroll
-        for (int m = 0; m < E; ++m) u[m] = cscale(u[m], buf_ld_f(gr, (uint32_t)e0 * 4u, (uint32_t)(G * m) * 4u));
-    }
+            for (int m = 0; m < E; ++m) u[m] = cscale(u[m], buf_ld_f(gr, (uint32_t)e0 * 4u, (uint32_t)(G * m) * 4u));
+        }
+    };
+    if constexpr (!kDmaIn<N, G, TIn>()) apply_gain();
     float2 hs[kEarly ? E : 1];
     if constexpr (kEarly) {
 #pragma unroll
         for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
+    }
+    if constexpr (kDmaIn<N, G, TIn>()) {   // the row has landed in the slot: to registers
+        pc_dma_read<TIn, N, G>(u, x + in_start, valid ? (uint32_t)in_len * ES : 0u, buf, t);
+        apply_gain();
     }
     // the FIR segment's staging loads ride on the same memory round trip (a second, dependent
     // round trip made the short rows' FIR phase ~40 % of their lifetime: tools/diag_stamps.py)
@@ -899,6 +958,7 @@ __device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nw
 // under the tile's FFT and Doppler CFAR instead of trailing the workgroup.
 struct RangeJob57 {
     static constexpr int H = 13, NX = 2 * H + 1;
+    static constexpr int kLoads = NX;   // fetch_cells' gathers (the hook of mtd_tile)
     uint32_t n = 0, idx = 0;
     float x[NX];
     __device__ __forceinline__ void fetch_idx(const MtdArgs& a, int rg) {
@@ -959,9 +1019,50 @@ struct RangeJob57 {
     }
 };
 
+struct RangeHook {   // mtd_tile's after_loads(): the range job's gathers
+    RangeJob57& rj;
+    const MtdArgs& a;
+    static constexpr int kLoads = RangeJob57::kLoads;
+    __device__ __forceinline__ void operator()() const { rj.fetch_cells(a); }
+};
+
 struct NoHook {
+    static constexpr int kLoads = 0;   // vector-memory operations operator() issues
     __device__ __forceinline__ void operator()() const {}
 };
+
+// MTD tile loads by LDS-DMA (dev-only -DRSP_MTD_DMA, A/B of VERDICT r3 item 1): one beam, no
+// MTI, default cache policy.  The tile's P rows of W complex columns (W*8 bytes each) go to LDS
+// as 16-byte pieces: a wave instruction covers 64/(W/2) whole rows; a lane past R_out (partial
+// right-edge tile) or a row past pin loads 0 through the range check.
+template <int P, int BEAMS, int LA, int W>
+__host__ __device__ constexpr bool kMtdDma() {
+#ifdef RSP_MTD_DMA
+    return BEAMS == 1 && LA == 0 && W >= 2 && W <= 128 && 64 % (W / 2) == 0;
+#else
+    return false;
+#endif
+}
+template <int P, int W, int T>
+__device__ __forceinline__ void mtd_dma_issue(__amdgpu_buffer_rsrc_t src, uint32_t col0, uint32_t R, unsigned char* smem) {
+    constexpr int LPR = W / 2;                    // lanes per row (16 B = 2 columns each)
+    constexpr int BYTES = P * W * 8;
+    constexpr int NQ = BYTES / (T * 16);          // DMA instructions per thread
+    static_assert(BYTES % (T * 16) == 0 && 64 % LPR == 0, "MTD DMA tiling");
+    const int t = threadIdx.x;
+    const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int piece = q * T + t;              // 16-byte piece of the linear [P][W] image
+        const int row = piece / LPR, cp = (piece % LPR) * 2;
+        // (no per-lane range test: a column past R_out of a right-edge tile reads the next
+        // row's first samples -- or 0 past the plane -- into an LDS column whose thread has
+        // rv == false, so nothing computed from it is stored; a select here made hipcc split
+        // every DMA into two exec-masked copies)
+        const uint32_t vo = ((uint32_t)row * R + col0 + (uint32_t)cp) * 8u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_void*)(smem + (q * T + wb) * 16), 16, vo, 0, 0, 0);
+    }
+}
 
 // MTD: one workgroup = W range bins x all P pulses.  Thread (c, g): range bin c of the
 // tile, pulses g + G*m (m < E) -- the strided pattern of fft_reg, so the pulse-compressed
@@ -1023,6 +1124,23 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
                 const float w = g + G * m + lag < pin ? a.win[g + G * m] : 0.f;
                 u[m] = make_float2((v1.x - v0.x) * w, (v1.y - v0.y) * w);
             }
+        } else if constexpr (kMtdDma<P, BEAMS, LA, W>()) {
+            // the tile's P rows x W columns land in LDS by DMA (row-major [p][c], linear), then
+            // thread (c, g) reads its strided pulses; the range job's gathers issue behind the
+            // DMA and stay in flight across the barrier (a counted vmcnt, a raw s_barrier)
+            float wv[E];
+#pragma unroll
+            for (int m = 0; m < E; ++m) wv[m] = a.win[g + G * m];
+            mtd_dma_issue<P, W, C::T>(src, (uint32_t)(T.bx * W), R, smem);
+            after_loads();
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Hook::kLoads) : "memory");
+            __builtin_amdgcn_s_barrier();
+            const float2* l = reinterpret_cast<const float2*>(smem);
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const float2 v = l[(g + G * m) * W + c];
+                u[m] = make_float2(v.x * wv[m], v.y * wv[m]);
+            }
         } else {
 #pragma unroll
             for (int m = 0; m < E; ++m) {
@@ -1031,7 +1149,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
                 u[m] = make_float2(v.x * w, v.y * w);
             }
         }
-        if (b == 0) after_loads();
+        if (b == 0 && !(kMtdDma<P, BEAMS, LA, W>() && a.mti_lag <= 0)) after_loads();
         RSP_STAMP(1, 1, true);
         fft_reg_w<P, G, 1, E, 0, NW>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, tw);
         RSP_STAMP(1, 2, false);
@@ -1184,7 +1302,7 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     RSP_STAMP(1, 0, false);
     RSP_STAMP_RT(1, 8);
     if (job) rj.fetch_idx(a, (int)wg);
-    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, [&] { rj.fetch_cells(a); });
+    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a});
     RSP_STAMP(1, 5, false);
     rj.finish(a);
     RSP_STAMP(1, 6, false);

@@ -29,7 +29,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
-           "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_ingest_record_bytes",
+           "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_set_host_pipeline", "rsp_ingest_record_bytes",
            "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter")
 RSP_NKERNELS = 4
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
@@ -138,6 +138,8 @@ def load_library(path=None):
     lib.rsp_set_streams.argtypes = [vp, i32]
     lib.rsp_set_pc_split.restype = C.c_int
     lib.rsp_set_pc_split.argtypes = [vp, i32]
+    lib.rsp_set_host_pipeline.restype = C.c_int
+    lib.rsp_set_host_pipeline.argtypes = [vp, i64, i32]
     lib.rsp_set_prefilter.restype = C.c_int
     lib.rsp_set_prefilter.argtypes = [vp, C.POINTER(C.c_float), i32]
     lib.rsp_ingest_record_bytes.restype = C.c_int

@@ -65,6 +65,11 @@ class Engine:
         whole-length transforms (0) -- rsp_set_pc_split."""
         capi.check(self.lib.rsp_set_pc_split(self.ctx, int(enable)), self.ctx)
 
+    def set_host_pipeline(self, cpis_per_chunk=0, copy_threads=0):
+        """Host-buffer calls (pc_mtd_cfar / pc_mtd): CPIs per pipelined chunk and host copy
+        threads (0 = the library defaults) -- rsp_set_host_pipeline."""
+        capi.check(self.lib.rsp_set_host_pipeline(self.ctx, int(cpis_per_chunk), int(copy_threads)), self.ctx)
+
     def set_prefilter(self, gain=None, mti_lag=0):
         """Fuse iSTC (gain: [R] linear gains, e.g. rsp.prefilter.istc_gain) into pulse
         compression's echo load and MTI (lag, e.g. 30) into the MTD's load of the PC rows

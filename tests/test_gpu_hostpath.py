@@ -1,0 +1,89 @@
+"""The pipelined host-buffer path (rsp_pc_mtd_cfar / rsp_pc_mtd with pageable host arrays, the
+MEX drop-in for MTD/main_produce_dataset_win_xzr_v2.m:136's one-CPI fun_MTD_produce calls):
+chunked H2D / chain / D2H through pinned staging rings must give exactly the device path's
+outputs -- whatever the chunking, the copy-thread count, the input dtype and the layouts
+(integer/layout work: bit-exact)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _engine(P, R):
+    from rsp import presets
+    from rsp.engine import Engine
+    return Engine(presets.v2(P, R), device=0)
+
+
+def _dev(torch, eng, echo64, cf):
+    """The device path on the same (complex64) samples: rdm, flag, flagV row-major."""
+    B = echo64.shape[0]
+    V, Ro = eng.shape
+    d = torch.from_numpy(echo64).cuda()
+    rdm = torch.empty((B, V, Ro), dtype=torch.float32, device="cuda")
+    flag = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+    fv = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+    eng.run_dev(d, rdm=rdm, flag=flag, flagV=fv, cfar=cf)
+    torch.cuda.synchronize()
+    return rdm.cpu().numpy(), flag.cpu().numpy(), fv.cpu().numpy()
+
+
+@pytest.mark.parametrize("P,R,batch,chunk,threads", [
+    (64, 1024, 7, 3, 0),      # 3 chunks, the last one short
+    (64, 1024, 1, 0, 0),      # MATLAB's granularity: one CPI per call
+    (64, 1024, 9, 1, 1),      # one CPI per chunk, one copy thread
+    (128, 4096, 11, 0, 0),    # by size: 32 MiB of C128 input = 4 CPIs per chunk, 3 chunks
+    (128, 4096, 1, 0, 5),     # one 8 MiB CPI: one pinned piece per direction plane
+])
+def test_host_path_equals_device_path(torch_cuda, P, R, batch, chunk, threads):
+    from rsp import _capi as capi
+    from rsp import presets, synth
+    eng = _engine(P, R)
+    cf = presets.default_cfar(eng.spec)
+    echo = synth.echo_numpy(eng.spec, batch, seed=77 + batch).astype(np.complex64)
+    want = _dev(torch_cuda, eng, echo, cf)
+    eng.set_host_pipeline(chunk, threads)
+    # MATLAB layout: complex double, column-major in and out
+    col = np.ascontiguousarray(np.swapaxes(echo.astype(np.complex128), 1, 2))
+    got = eng.pc_mtd_cfar(col, cf, layout=capi.RSP_COLMAJOR, out_layout=capi.RSP_COLMAJOR)
+    for g, w in zip(got, want):
+        assert np.array_equal(np.swapaxes(g, 1, 2), w)
+    # row-major complex64 in and out, without flagV
+    rdm, flag, fv = eng.pc_mtd_cfar(echo, cf, want_flagV=False)
+    assert fv is None and np.array_equal(rdm, want[0]) and np.array_equal(flag, want[1])
+    # PC + MTD only
+    assert np.array_equal(eng.pc_mtd(echo), want[0])
+    eng.close()
+
+
+def test_host_path_repeated_calls_and_fp16(torch_cuda):
+    """Back-to-back calls reuse the rings and slots (events from the previous call) and the
+    fp16 I/Q input goes through the same pipeline."""
+    torch = torch_cuda
+    from rsp import presets, synth
+    eng = _engine(64, 2048)
+    cf = presets.default_cfar(eng.spec)
+    eng.set_host_pipeline(2, 0)
+    for seed in (1, 2, 3):
+        echo = synth.echo_numpy(eng.spec, 5, seed=seed).astype(np.complex64)
+        want = _dev(torch, eng, echo, cf)
+        got = eng.pc_mtd_cfar(echo, cf)
+        for g, w in zip(got, want):
+            assert np.array_equal(g, w)
+    echo = synth.echo_numpy(eng.spec, 3, seed=9).astype(np.complex64)
+    iq = np.ascontiguousarray(np.stack([echo.real, echo.imag], axis=-1).astype(np.float16))   # [3, P, R, 2]
+    V, Ro = eng.shape
+    rdm = torch.empty((3, V, Ro), dtype=torch.float32, device="cuda")
+    flag = torch.empty((3, V, Ro), dtype=torch.uint8, device="cuda")
+    eng.run_dev(torch.from_numpy(iq).cuda(), rdm=rdm, flag=flag, cfar=cf)
+    torch.cuda.synchronize()
+    got = eng.pc_mtd_cfar(iq, cf, want_flagV=False)
+    assert np.array_equal(got[0], rdm.cpu().numpy()) and np.array_equal(got[1], flag.cpu().numpy())
+    eng.close()

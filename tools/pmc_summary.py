@@ -32,21 +32,34 @@ def short(name):
 
 
 def load(pmc_dir):
+    """Per kernel: counter -> values, and the dispatch durations (us) of the FETCH_SIZE pass and
+    of the pass that carried GRBM_GUI_ACTIVE (each counter is normalised by its own pass)."""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
+    dur_grbm = collections.defaultdict(list)
     for f in sorted(glob.glob(os.path.join(pmc_dir, "g*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             if r["Counter_Name"] in ("FETCH_SIZE",):
-                dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    return acc, dur
+                dur[k].append(us)
+            if r["Counter_Name"] in ("GRBM_GUI_ACTIVE",):
+                dur_grbm[k].append(us)
+    return acc, dur, dur_grbm
+
+
+# GRBM_GUI_ACTIVE counts the busy cycles of a dispatch's sampling window, summed over the 8 XCDs;
+# the window exceeds the kernel by a roughly fixed launch overhead, so GRBM/8/duration reads high
+# on short dispatches (MI355X_MICROARCH.md, DVFS give-back: within 3 % only from ~10 ms, high
+# below ~0.3 ms).  The clock is reported only for dispatches of at least this length.
+MIN_CLOCK_US = 300.0
 
 
 def main():
     args = sys.argv[1:]
     pmc_dir = args[0] if args and not args[0].startswith("--") else "gpurun_out/pmc"
-    acc, dur = load(pmc_dir)
+    acc, dur, dur_grbm = load(pmc_dir)
     rows = {}
     for k, cs in acc.items():
         if not any(x in k for x in ("pc_", "mtd", "cfar", "memset", "hits_kernel", "measure_kernel", "prefilter_kernel", "mti_chain", "ingest")):
@@ -70,8 +83,14 @@ def main():
                 row[c] = m[c]
         if "TCC_HIT_sum" in m:
             row["L2_hit"] = round(m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 3)
-        if "GRBM_GUI_ACTIVE" in m and d == d and d > 0:
-            row["eff_clock_GHz"] = round(m["GRBM_GUI_ACTIVE"] / 8 / (d * 1e3), 3)
+        if "GRBM_GUI_ACTIVE" in m and dur_grbm[k]:
+            dg = sum(dur_grbm[k]) / len(dur_grbm[k])   # the GRBM pass's own dispatch durations
+            row["grbm_pass_avg_us"] = round(dg, 2)
+            if dg >= MIN_CLOCK_US:
+                row["eff_clock_GHz"] = round(m["GRBM_GUI_ACTIVE"] / 8 / (dg * 1e3), 3)
+            else:
+                row["eff_clock_GHz"] = None
+                row["eff_clock_note"] = "dispatch < %.0f us: the GRBM sampling window exceeds the kernel" % MIN_CLOCK_US
         if "SQ_WAVE_CYCLES" in m and "SQ_WAIT_ANY" in m:
             wc = m["SQ_WAVE_CYCLES"]
             row["wait_frac"] = round(m["SQ_WAIT_ANY"] / wc, 3)
