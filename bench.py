@@ -639,13 +639,23 @@ def device_identity(local, dry=False, force=-1):
             "name": getattr(pr, "gcnArchName", None) or pr.name}
 
 
+def device_key(d):
+    """One GPU's identity: its UUID, else its PCI address, else (visible devices, local index)."""
+    if d.get("uuid") is not None:
+        return "uuid:" + str(d["uuid"])
+    if d.get("pci") is not None:
+        return "pci:" + str(d["pci"])
+    return "local:%s/%s" % (d.get("visible"), d.get("local"))
+
+
 def duplicate_devices(idents):
     """Pairs of ranks whose identities name one physical GPU (same UUID, or same PCI address)."""
     dup = []
     for i in range(len(idents)):
         for j in range(i + 1, len(idents)):
             a, b = idents[i], idents[j]
-            if any(a.get(k) is not None and a.get(k) == b.get(k) for k in ("uuid", "pci")):
+            if any(a.get(k) is not None and a.get(k) == b.get(k) for k in ("uuid", "pci")) or \
+                    device_key(a) == device_key(b):
                 dup.append((i, j))
     return dup
 
@@ -704,7 +714,7 @@ def dry_run(args, world, rank, dist):
             "vs_baseline": None, "dry_run": True, "config": {"workload": args.config, "batch_per_gpu": args.batch},
             "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank], "shards": plans,
             "collectives": dist.get_backend() if world > 1 else None,
-            "distinct_devices": len({(p["device"].get("uuid"), p["device"].get("pci")) for p in plans})}), flush=True)
+            "distinct_devices": len({device_key(p["device"]) for p in plans})}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -941,7 +951,7 @@ def main():
                        "parallelism": ("%d ranks sharing device 0 (launcher rehearsal, not a scaling result)" % world
                                        if args.share_device else "frame-sharded x%d, no data-path collective "
                                        "(gloo host barrier/gathers only)" % world)},
-            "distinct_devices": len({(d["device"].get("uuid"), d["device"].get("pci")) for d in plans}),
+            "distinct_devices": len({device_key(d["device"]) for d in plans}),
             "collectives": dist.get_backend() if world > 1 else None,
             "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank],
             "shards": plans,

@@ -20,6 +20,8 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rsp_fft.h"
 #include "rsp_buf.h"
 #include "rsp_internal.h"
@@ -305,7 +307,7 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
 // elements re-read by the lane that owns it before the barrier.
 template <int N, int G, typename TIn>
 __host__ __device__ constexpr bool kDmaIn() {
-#ifdef RSP_PC_DMA
+#if defined(RSP_PC_DMA) && RSP_PC_DMA == 1
     return G >= 256 && G % 64 == 0 && (N * (int)sizeof(TIn)) % (G * 16) == 0;
 #else
     return false;
@@ -489,6 +491,154 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     RSP_STAMP_RT(0, 9);
 }
 
+#if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
+// Persistent long rows with an LDS-DMA prefetch ring (dev-only -DRSP_PC_DMA=2, A/B of VERDICT r3
+// item 1, variant "persistent grid, 2-slot LDS ring"): each workgroup owns two padded row slots
+// (2 workgroups per CU) and walks rows first, first + step, ...  Row k computes in slot k % 2
+// while row k+1's input lands in the other slot by buffer_load_dwordx4 ... lds, issued right
+// after the barrier that opens row k.  The DMA and the spectrum loads are inline asm, invisible
+// to hipcc's waitcnt pass (a compiler-visible LDS-DMA makes every later barrier or LDS fence
+// wait vmcnt(0), draining the prefetch), so every wait on them is counted here by hand: the
+// only compiler-visible VMEM operations inside the loop are the row's stores.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i_t rsrc_words(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    v4i_t r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    r.y = __builtin_amdgcn_readfirstlane((int)((p >> 32) & 0xffffu));
+    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+__device__ __forceinline__ void dma16_asm(v4i_t rs, uint32_t voff, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rs), "s"(lds_byte)
+                 : "memory");
+}
+__device__ __forceinline__ float2 ld8_asm(v4i_t rs, uint32_t voff, uint32_t soff) {
+    float2 v;
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rs), "s"(soff) : "memory");
+    return v;
+}
+// s_waitcnt vmcnt(K) that also (re)defines the registers an asm load wrote, so no use of them is
+// scheduled above the wait
+template <int K>
+__device__ __forceinline__ void vm_wait16(float2 (&h)[16]) {
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]), "+v"(h[7]),
+                   "+v"(h[8]), "+v"(h[9]), "+v"(h[10]), "+v"(h[11]), "+v"(h[12]), "+v"(h[13]), "+v"(h[14]), "+v"(h[15])
+                 : "n"(K)
+                 : "memory");
+}
+template <int K>
+__device__ __forceinline__ void vm_wait1(float2& x) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x) : "n"(K) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_byte(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int N, int G>
+__device__ __forceinline__ void pc_long_persist(const float2* __restrict__ echo, float2* __restrict__ out,
+                                                const PcMfArgs& a, int first, int step, float2* lds) {
+    constexpr int E = N / G;
+    static_assert(E == 16 && G % 64 == 0, "persistent PC rows: 16 elements per thread, whole waves");
+    constexpr int SLOT = padded_len(N);
+    constexpr int NQ = N * 8 / (G * 16);   // DMA pieces per thread per row
+    const int t = threadIdx.x;
+    const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
+    const int ns = a.nsub > 1 ? a.nsub : 1;
+    const int nun = a.rows * ns;
+    constexpr int NW = tw_regs<N, E>() > 0 ? tw_regs<N, E>() : 1;
+    float2 w[NW];
+    tw_preload<N, G, 1, E, 0, NW>(w, t, a.mf.tw);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[i]) : : "memory");
+    const v4i_t rh = rsrc_words(a.mf.H, (uint32_t)N * 8u);
+    struct Geo {
+        const float2* x;
+        float2* y;
+        uint32_t in_bytes, out_bytes;
+    };
+    auto geo = [&](int u) {
+        const int row = __builtin_amdgcn_readfirstlane(u / ns), sub = __builtin_amdgcn_readfirstlane(u % ns);
+        int in_start = a.mf.in_start, in_len = a.mf.in_len, out_start = a.mf.out_start, out_len = a.mf.out_len;
+        if (a.nsub > 1) {
+            const int off = sub * a.sub_step;
+            in_start += off;
+            out_start += off;
+            in_len = max(0, min(in_len - off, N));
+            out_len = max(0, min(out_len - off, a.sub_step));
+        }
+        Geo g;
+        g.x = echo + (size_t)row * a.R + __builtin_amdgcn_readfirstlane(in_start);
+        g.y = out + (size_t)row * a.R_out + __builtin_amdgcn_readfirstlane(out_start);
+        g.in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(in_len) * 8u;
+        g.out_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(out_len) * 8u;
+        return g;
+    };
+    // a row's input: NQ pieces into `slot` (16-byte pieces, rsrc cut at a 16-byte boundary) and
+    // the straddling element (an odd in_len) by the lane owning its piece, into a register
+    auto issue = [&](const Geo& g, float2* slot, float2& strad) {
+        const uint32_t nb16 = g.in_bytes & ~15u;
+        const v4i_t rx = rsrc_words(g.x, nb16);
+        const uint32_t base = lds_byte(slot);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) dma16_asm(rx, (uint32_t)(q * G + t) * 16u, base + (uint32_t)(q * G + wb) * 16u);
+        const v4i_t rs = rsrc_words(g.x, g.in_bytes);
+        const bool own = nb16 < g.in_bytes && (nb16 / 16u) % (uint32_t)G == (uint32_t)t;
+        strad = ld8_asm(rs, own ? nb16 : kOob, 0u);
+    };
+    // (slot k is lds + k * SLOT -- an offset from the LDS array, so the accesses stay ds_*: a
+    // pointer picked from an array of two made hipcc fall back to flat loads and stores)
+    int k = 0;
+    Geo g = geo(first < nun ? first : 0);
+    float2 strad = make_float2(0.f, 0.f);
+    if (first < nun) issue(g, lds, strad);
+    bool head = true;
+    for (int u = first; u < nun; u += step, k ^= 1) {
+        float2 hs[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) hs[m] = ld8_asm(rh, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+        // this row's pieces and patch are older than: (not the first row) the previous row's
+        // E stores, and the E spectrum loads just issued
+        if (head) vm_wait1<E>(strad);
+        else vm_wait1<2 * E>(strad);
+        head = false;
+        float2* cur = lds + k * SLOT;
+        {
+            const uint32_t nb16 = g.in_bytes & ~15u;
+            if (nb16 < g.in_bytes && (nb16 / 16u) % (uint32_t)G == (uint32_t)t) cur[nb16 / 8u] = strad;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // every wave is past the previous row (its last reads of the other slot) and this row
+        // has landed: prefetch the next row into the other slot
+        const Geo gr = g;
+        const bool more = u + step < nun;
+        if (more) {
+            g = geo(u + step);
+            issue(g, lds + (k ^ 1) * SLOT, strad);
+        }
+        float2 v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = cur[t + G * m];
+        fft_reg_w<N, G, 1, E, 0, NW, false>(v, cur, t, w);
+        // the spectrum loads are older than the next row's NQ pieces and patch load
+        if (more) vm_wait16<NQ + 1>(hs);
+        else vm_wait16<0>(hs);
+#pragma unroll
+        for (int m = 0; m < E; m += 2) cmul2_conj(v[m], v[m], hs[m], v[m + 1], v[m + 1], hs[m + 1]);
+        fft_reg_w<N, G, 1, E, 0, NW, false>(v, cur, t, w);
+        const auto yr = buf_rsrc(gr.y, gr.out_bytes);
+#pragma unroll
+        for (int m = 0; m < E; ++m) buf_st_f2(cconj(v[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
+    }
+}
+#endif
+
 // Workgroup size shared by a pair of segment lengths: both run T threads (RPB = T/G rows).
 template <int N1, int N2>
 struct PairCfg {
@@ -510,6 +660,17 @@ __device__ __forceinline__ void pc_mf_block(const TIn* __restrict__ echo, float2
     using PC = PairCfg<N1, M2>;
     // unit u of a segment = (row u / nsub, overlap-save sub-block u % nsub)
     if constexpr (N2 != 0) {
+#if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
+        if constexpr (std::is_same<TIn, float2>::value && PcCfg<N2>::G == PC::T && N2 <= 4096) {
+            if (nblk2 < 0) {   // the host chose the persistent form: -nblk2 workgroups walk the long rows
+                if (bid < -nblk2) {
+                    pc_long_persist<N2, PcCfg<N2>::G>(echo, out, a2, bid, -nblk2, lds);
+                    return;
+                }
+                nblk2 = -nblk2;
+            }
+        }
+#endif
         if (bid < nblk2) {
             constexpr int G = PcCfg<N2>::G;
             const int grp = threadIdx.x / G, t = threadIdx.x % G;
@@ -579,6 +740,27 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds + RSP_DIAG_PC_LDS_EXTRA, s, echo, out, a1,
                        a2 ? *a2 : a1, nblk2);
     return hipGetLastError();
+#endif
+#if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
+    if constexpr (std::is_same<TIn, float2>::value && N2 != 0 && N2 <= 4096 && PcCfg<M2>::G == PC::T) {
+        if (a2 && a2->gain == nullptr && nblk2 > 0) {   // persistent long rows: 2 workgroups per CU
+            static int cus = 0;
+            if (!cus) {
+                int dev = 0;
+                if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+                if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorInvalidDevice;
+            }
+            const int nper = u2 < 2 * cus ? u2 : 2 * cus;
+            constexpr size_t L2X = 2 * (size_t)PcCfg<M2>::SLOT * sizeof(float2);
+            constexpr size_t LX = L2X > PC::lds ? L2X : PC::lds;
+            static LaunchOnce once_p;
+            e = lds_attr(once_p, (const void*)pc_mf_kernel<TIn, N1, N2>, LX);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), dim3((unsigned)(nblk1 + nper)), block, LX, s, echo, out, a1,
+                               *a2, -nper);
+            return hipGetLastError();
+        }
+    }
 #endif
     hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds, s, echo, out, a1,
                        a2 ? *a2 : a1, nblk2);

@@ -86,4 +86,6 @@ def test_duplicate_device_check_unit():
     assert bench.duplicate_devices([a, b]) == []
     assert bench.duplicate_devices([a, b, dict(a, local=2)]) == [(0, 2)]
     assert bench.duplicate_devices([a, dict(b, uuid=None, pci="0000:05:00")]) == [(0, 1)]
+    # neither UUID nor PCI address: the local index (under the same device visibility) decides
     assert bench.duplicate_devices([dict(a, uuid=None, pci=None), dict(b, uuid=None, pci=None)]) == []
+    assert bench.duplicate_devices([dict(a, uuid=None, pci=None), dict(a, uuid=None, pci=None)]) == [(0, 1)]
