@@ -24,32 +24,12 @@
 
 #include "rsp_fft.h"
 #include "rsp_buf.h"
+#include "rsp_diag.h"
 #include "rsp_internal.h"
 
 
 namespace rsp {
 
-#ifdef RSP_DIAG_STAMPS
-// Dev-only diagnostic build (tools/build_variant.sh, read by tools/diag_stamps.py): per-workgroup
-// phase timestamps of the PC and MTD kernels.  Lane 0 of wave 0 writes the shader clock
-// (s_memtime) at a phase boundary into an array no other code reads; a boundary marked `wait`
-// first waits for the wave's own memory operations, so "loads arrived" / "stores done" are
-// points in time.  Slots 8 and 9 hold the 100 MHz real-time clock at entry and exit; 10-12
-// split the FIR (staged, computed, stored).
-constexpr int kDiagSlots = 16, kDiagWG = 1 << 15;
-__device__ uint64_t g_diag[2][kDiagWG * kDiagSlots];
-__device__ __forceinline__ void diag_stamp(int k, int slot, bool wait, bool realtime = false) {
-    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint64_t t = realtime ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
-    const uint32_t wg = blockIdx.x + blockIdx.y * gridDim.x;
-    if (threadIdx.x == 0 && wg < (uint32_t)kDiagWG) g_diag[k][wg * kDiagSlots + slot] = t;
-}
-#define RSP_STAMP(k, slot, wait) diag_stamp(k, slot, wait)
-#define RSP_STAMP_RT(k, slot) diag_stamp(k, slot, false, true)
-#else
-#define RSP_STAMP(k, slot, wait) ((void)0)
-#define RSP_STAMP_RT(k, slot) ((void)0)
-#endif
 
 __device__ __forceinline__ float2 ld_c(const float2* p) { return *p; }
 __device__ __forceinline__ float2 ld_c(const __half2* p) { return __half22float2(*p); }
@@ -371,16 +351,8 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         sub = __builtin_amdgcn_readfirstlane(sub);
     }
     const bool valid = row < a.rows;
-#ifdef RSP_DIAG_PC_L2IN   // dev-only diagnostic build (tools/build_variant.sh): rows read 64 L2-resident inputs
-    const TIn* x = echo + (size_t)(row & 63) * a.R;
-#else
-    const TIn* x = echo + (size_t)row * a.R;
-#endif
-#ifdef RSP_DIAG_PC_NOSTORE   // dev-only diagnostic build: every output store range-checked away
-    const bool st_ok = valid && a.rows < 0;
-#else
-    const bool st_ok = valid;
-#endif
+    const TIn* x = echo + (size_t)diag_pc_src_row(row) * a.R;
+    const bool st_ok = valid && !kDiagPcNoStore;
     float2* y = out + (size_t)row * a.R_out;
     int in_start = a.mf.in_start, in_len = a.mf.in_len;
     int out_start = a.mf.out_start, out_len = a.mf.out_len;
@@ -450,9 +422,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
                                 kUniform ? fpre : nullptr);
     }
     RSP_STAMP(0, 2, false);
-#ifndef RSP_DIAG_PC_NOFFT   // dev-only diagnostic build: load, spectrum multiply, store (no FFTs)
-    fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
-#endif
+    if constexpr (!kDiagPcNoFft) fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
     RSP_STAMP(0, 3, false);
     if constexpr (kEarly) {
 #pragma unroll
@@ -471,9 +441,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         }
     }
     RSP_STAMP(0, 4, false);
-#ifndef RSP_DIAG_PC_NOFFT
-    fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
-#endif
+    if constexpr (!kDiagPcNoFft) fft_reg_w<N, G, 1, E, 0, NW, WS>(u, buf, t, w);
     RSP_STAMP(0, 5, false);
     if constexpr (kUniform) {
         const auto yr = buf_rsrc(y + out_start, st_ok ? (uint32_t)out_len * 8u : 0u);
@@ -689,9 +657,6 @@ __device__ __forceinline__ void pc_mf_block(const TIn* __restrict__ echo, float2
     pc_row<TIn, N1, G, 0, G == 64>(echo, out, a1, u / ns, t, lds + grp * PcCfg<N1>::SLOT, u % ns);
 }
 
-#ifndef RSP_DIAG_PC_WAVES   // dev-only diagnostic build: minimum waves per SIMD of the PC kernel
-#define RSP_DIAG_PC_WAVES 2
-#endif
 template <typename TIn, int N1, int N2>
 __global__ __launch_bounds__((PairCfg<N1, (N2 ? N2 : N1)>::T), RSP_DIAG_PC_WAVES) void pc_mf_kernel(
     const TIn* __restrict__ echo, float2* __restrict__ out, PcMfArgs a1, PcMfArgs a2, int nblk2) {
@@ -726,21 +691,14 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
     static LaunchOnce once;
-    hipError_t e = lds_attr(once, (const void*)pc_mf_kernel<TIn, N1, N2>, PC::lds);
+    constexpr size_t lds = PC::lds + kDiagPcLdsExtra;
+    hipError_t e = lds_attr(once, (const void*)pc_mf_kernel<TIn, N1, N2>, lds);
     if (e != hipSuccess) return e;
     const int u1 = a1.rows * (a1.nsub > 1 ? a1.nsub : 1);
     const int nblk1 = (u1 + PC::RPB1 - 1) / PC::RPB1;
     const int u2 = a2 ? a2->rows * (a2->nsub > 1 ? a2->nsub : 1) : 0;
     const int nblk2 = N2 ? (u2 + PC::RPB2 - 1) / PC::RPB2 : 0;
     dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
-#ifdef RSP_DIAG_PC_LDS_EXTRA   // dev-only diagnostic build: extra dynamic LDS to cap workgroups per CU
-    static LaunchOnce once_x;
-    e = lds_attr(once_x, (const void*)pc_mf_kernel<TIn, N1, N2>, PC::lds + RSP_DIAG_PC_LDS_EXTRA);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds + RSP_DIAG_PC_LDS_EXTRA, s, echo, out, a1,
-                       a2 ? *a2 : a1, nblk2);
-    return hipGetLastError();
-#endif
 #if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
     if constexpr (std::is_same<TIn, float2>::value && N2 != 0 && N2 <= 4096 && PcCfg<M2>::G == PC::T) {
         if (a2 && a2->gain == nullptr && nblk2 > 0) {   // persistent long rows: 2 workgroups per CU
@@ -762,8 +720,7 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
         }
     }
 #endif
-    hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, PC::lds, s, echo, out, a1,
-                       a2 ? *a2 : a1, nblk2);
+    hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, lds, s, echo, out, a1, a2 ? *a2 : a1, nblk2);
     return hipGetLastError();
 }
 
