@@ -282,9 +282,9 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
 // samples go global -> its LDS exchange slot by `buffer_load_dwordx4 ... lds` (16 B per lane, 1 KiB
 // contiguous per wave instruction, no VGPR destination), then each thread reads its strided
 // elements u[m] = x[t + G*m] from the slot (lane-contiguous ds_read_b64: conflict-free).  The
-// buffer range check supplies the zero padding past in_len; the 16-byte access that straddles
-// in_len is dropped whole by the rsrc (num_records rounded down to 16 B) and its in-range
-// elements re-read by the lane that owns it before the barrier.
+// buffer range check supplies the zero padding past in_len; it is per dword on gfx950, also for
+// LDS-DMA (tools/micro/lds_dma_probe.hip), so a 16-byte piece that straddles in_len keeps its
+// in-range elements.
 template <int N, int G, typename TIn>
 __host__ __device__ constexpr bool kDmaIn() {
 #if defined(RSP_PC_DMA) && RSP_PC_DMA == 1
@@ -298,7 +298,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 template <typename TIn, int N, int G>
 __device__ __forceinline__ void pc_dma_issue(const TIn* x, uint32_t nbytes, float2* slot, int t) {
     constexpr int NQ = N * (int)sizeof(TIn) / (G * 16);
-    const auto xr = buf_rsrc(x, nbytes & ~15u);
+    const auto xr = buf_rsrc(x, nbytes);
     const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
     char* l = reinterpret_cast<char*>(slot);
 #pragma unroll
@@ -308,20 +308,9 @@ __device__ __forceinline__ void pc_dma_issue(const TIn* x, uint32_t nbytes, floa
 }
 
 template <typename TIn, int N, int G>
-__device__ __forceinline__ void pc_dma_read(float2 (&u)[N / G], const TIn* x, uint32_t nbytes, float2* slot, int t) {
+__device__ __forceinline__ void pc_dma_read(float2 (&u)[N / G], float2* slot, int t) {
     constexpr int E = N / G;
-    constexpr uint32_t ES = sizeof(TIn);
-    // the straddling 16 bytes [nb16, nb16 + 16) hold (nbytes - nb16) / ES in-range elements
-    const uint32_t nb16 = nbytes & ~15u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (nb16 < nbytes && (uint32_t)(nb16 / 16u) % G == (uint32_t)t) {
-        const auto xr = buf_rsrc(x, nbytes);
-        TIn* l = reinterpret_cast<TIn*>(slot);
-        for (uint32_t o = nb16; o < nbytes; o += ES) {
-            if constexpr (ES == 8) l[o / ES] = buf_ld_f2(xr, o, 0u);
-            else l[o / ES] = __builtin_bit_cast(TIn, __builtin_amdgcn_raw_buffer_load_b32(xr, o, 0u, 0));
-        }
-    }
     __syncthreads();
     const TIn* l = reinterpret_cast<const TIn*>(slot);
 #pragma unroll
@@ -404,7 +393,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
         for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
     }
     if constexpr (kDmaIn<N, G, TIn>()) {   // the row has landed in the slot: to registers
-        pc_dma_read<TIn, N, G>(u, x + in_start, valid ? (uint32_t)in_len * ES : 0u, buf, t);
+        pc_dma_read<TIn, N, G>(u, buf, t);
         apply_gain();
     }
     // the FIR segment's staging loads ride on the same memory round trip (a second, dependent
@@ -501,10 +490,7 @@ __device__ __forceinline__ void vm_wait16(float2 (&h)[16]) {
                  : "n"(K)
                  : "memory");
 }
-template <int K>
-__device__ __forceinline__ void vm_wait1(float2& x) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x) : "n"(K) : "memory");
-}
+
 __device__ __forceinline__ uint32_t lds_byte(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -548,39 +534,30 @@ __device__ __forceinline__ void pc_long_persist(const float2* __restrict__ echo,
         g.out_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(out_len) * 8u;
         return g;
     };
-    // a row's input: NQ pieces into `slot` (16-byte pieces, rsrc cut at a 16-byte boundary) and
-    // the straddling element (an odd in_len) by the lane owning its piece, into a register
-    auto issue = [&](const Geo& g, float2* slot, float2& strad) {
-        const uint32_t nb16 = g.in_bytes & ~15u;
-        const v4i_t rx = rsrc_words(g.x, nb16);
+    // a row's input: NQ 16-byte pieces into `slot` (the range check is per dword, so a piece
+    // straddling in_len keeps its in-range element)
+    auto issue = [&](const Geo& g, float2* slot) {
+        const v4i_t rx = rsrc_words(g.x, g.in_bytes);
         const uint32_t base = lds_byte(slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) dma16_asm(rx, (uint32_t)(q * G + t) * 16u, base + (uint32_t)(q * G + wb) * 16u);
-        const v4i_t rs = rsrc_words(g.x, g.in_bytes);
-        const bool own = nb16 < g.in_bytes && (nb16 / 16u) % (uint32_t)G == (uint32_t)t;
-        strad = ld8_asm(rs, own ? nb16 : kOob, 0u);
     };
     // (slot k is lds + k * SLOT -- an offset from the LDS array, so the accesses stay ds_*: a
     // pointer picked from an array of two made hipcc fall back to flat loads and stores)
     int k = 0;
     Geo g = geo(first < nun ? first : 0);
-    float2 strad = make_float2(0.f, 0.f);
-    if (first < nun) issue(g, lds, strad);
+    if (first < nun) issue(g, lds);
     bool head = true;
     for (int u = first; u < nun; u += step, k ^= 1) {
         float2 hs[E];
 #pragma unroll
         for (int m = 0; m < E; ++m) hs[m] = ld8_asm(rh, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-        // this row's pieces and patch are older than: (not the first row) the previous row's
-        // E stores, and the E spectrum loads just issued
-        if (head) vm_wait1<E>(strad);
-        else vm_wait1<2 * E>(strad);
+        // this row's pieces are older than: (not the first row) the previous row's E stores, and
+        // the E spectrum loads just issued
+        if (head) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * E) : "memory");
         head = false;
         float2* cur = lds + k * SLOT;
-        {
-            const uint32_t nb16 = g.in_bytes & ~15u;
-            if (nb16 < g.in_bytes && (nb16 / 16u) % (uint32_t)G == (uint32_t)t) cur[nb16 / 8u] = strad;
-        }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         // every wave is past the previous row (its last reads of the other slot) and this row
         // has landed: prefetch the next row into the other slot
@@ -588,14 +565,14 @@ __device__ __forceinline__ void pc_long_persist(const float2* __restrict__ echo,
         const bool more = u + step < nun;
         if (more) {
             g = geo(u + step);
-            issue(g, lds + (k ^ 1) * SLOT, strad);
+            issue(g, lds + (k ^ 1) * SLOT);
         }
         float2 v[E];
 #pragma unroll
         for (int m = 0; m < E; ++m) v[m] = cur[t + G * m];
         fft_reg_w<N, G, 1, E, 0, NW, false>(v, cur, t, w);
-        // the spectrum loads are older than the next row's NQ pieces and patch load
-        if (more) vm_wait16<NQ + 1>(hs);
+        // the spectrum loads are older than the next row's NQ pieces
+        if (more) vm_wait16<NQ>(hs);
         else vm_wait16<0>(hs);
 #pragma unroll
         for (int m = 0; m < E; m += 2) cmul2_conj(v[m], v[m], hs[m], v[m + 1], v[m + 1], hs[m + 1]);
@@ -1271,6 +1248,9 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 #pragma unroll
             for (int m = 0; m < E; ++m) wv[m] = a.win[g + G * m];
             mtd_dma_issue<P, W, C::T>(src, (uint32_t)(T.bx * W), R, smem);
+            // (a compiler barrier: the range gathers below must issue after every DMA piece, or
+            // the counted vmcnt would not cover the pieces -- hipcc interleaved them otherwise)
+            asm volatile("" ::: "memory");
             after_loads();
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Hook::kLoads) : "memory");
             __builtin_amdgcn_s_barrier();

@@ -114,9 +114,10 @@ class Engine:
         return int(np.prod(echo_shape[:-2])) if len(echo_shape) > 2 else 1
 
     def pc_mtd_cfar(self, echo, cfar=None, layout=capi.RSP_ROWMAJOR, out_layout=capi.RSP_ROWMAJOR,
-                    want_flagV=True):
+                    want_flagV=True, out=None):
         """echo: [batch][P][R] complex (row-major) or MATLAB [batch][R][P] with layout=COLMAJOR.
-        Returns rdm (float32) [, flag, flagV (uint8)] in out_layout."""
+        Returns rdm (float32) [, flag, flagV (uint8)] in out_layout; `out` = (rdm, flag, flagV)
+        host arrays to fill instead of fresh ones (flag / flagV may be None)."""
         a, dt = self._echo_host(echo, layout)
         shape = a.shape if dt != capi.RSP_C32F16 else a.shape[:-1]
         batch = self._batch_dims(shape, layout)
@@ -125,13 +126,19 @@ class Engine:
         batch //= self.spec.beams
         P, Ro, V = self.spec.P, self.spec.R_out, self.spec.V
         oshape = (batch, V, Ro) if out_layout == capi.RSP_ROWMAJOR else (batch, Ro, V)
-        rdm = np.empty(oshape, np.float32)
+        rdm = np.empty(oshape, np.float32) if out is None else out[0]
         flag = flagV = None
         cp = None
         if cfar is not None:
             cp = cfar.to_c()
-            flag = np.empty(oshape, np.uint8)
-            flagV = np.empty(oshape, np.uint8) if want_flagV else None
+            if out is None:
+                flag = np.empty(oshape, np.uint8)
+                flagV = np.empty(oshape, np.uint8) if want_flagV else None
+            else:
+                flag, flagV = out[1], out[2]
+        for o, dt in ((rdm, np.float32), (flag, np.uint8), (flagV, np.uint8)):
+            if o is not None and (o.shape != oshape or o.dtype != dt or not o.flags.c_contiguous):
+                raise ValueError("output arrays must be C-contiguous %s of shape %s" % (dt.__name__, oshape))
         rc = self.lib.rsp_pc_mtd_cfar(self.ctx, _ptr(a), dt, layout, P, self.spec.R, batch,
                                       C.byref(cp) if cp is not None else None, _ptr(rdm), out_layout,
                                       _ptr(flag), _ptr(flagV))

@@ -96,6 +96,12 @@ def main():
             row["wait_frac"] = round(m["SQ_WAIT_ANY"] / wc, 3)
             row["valu_frac"] = round(m.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3)
             row["lds_frac"] = round(m.get("SQ_ACTIVE_INST_LDS", 0) / wc, 3)
+            if "SQ_WAIT_INST_ANY" in m:   # issue stalls (dependency / pipe busy), disjoint from WAIT_ANY
+                row["issue_stall_frac"] = round(m["SQ_WAIT_INST_ANY"] / wc, 3)
+            if "SQ_ACTIVE_INST_ANY" in m:
+                row["active_frac"] = round(m["SQ_ACTIVE_INST_ANY"] / wc, 3)
+            if "SQ_INSTS_VALU" in m and m.get("SQ_WAVES"):
+                row["valu_insts_per_wave"] = round(m["SQ_INSTS_VALU"] / m["SQ_WAVES"], 1)
         rows[k] = row
     for k, r in rows.items():
         print(k)

@@ -22,4 +22,6 @@ timeout -k 10 200 python bench.py --steps 5 --cpu-seconds 0 --host-path --lane-s
 tail -1 gpurun_out/host_c3.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3', d['value'], 'host', json.dumps(d.get('host_path')))"
 timeout -k 10 240 $M/hbm_ceiling 2 > gpurun_out/hbm_ceiling.txt 2>&1 || { echo "ceiling failed"; exit 1; }
 tail -1 gpurun_out/hbm_ceiling.txt
+timeout -k 10 120 python tools/mall_probe.py > gpurun_out/mall_probe.txt 2>&1 || { echo "mall probe failed"; exit 1; }
+grep cpis gpurun_out/mall_probe.txt
 VARIANTS="${VARIANTS:-base dma1 dma2 mdma}" CONFIGS="${CONFIGS:-c3}" REPS=${REPS:-2} timeout -k 10 700 tools/ab2.sh
