@@ -1381,7 +1381,7 @@ static int check_host_call(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_
 
 // ---- pipelined host path
 static constexpr size_t kHostPiece = 8u << 20;        // pinned piece
-static constexpr size_t kHostChunkBytes = 32u << 20;  // input bytes per host chunk
+static constexpr size_t kHostChunkBytes = 32u << 20;  // caller's input bytes per host chunk
 
 static int host_pipe_init(rsp_ctx* ctx) {
     auto& h = ctx->hp;
@@ -1416,15 +1416,30 @@ static rsp::CopyPool& host_pool(rsp_ctx* ctx) {
 
 // host (pageable) -> device, through the pinned input ring on the H2D stream: piece i is
 // copied into a ring slot by the pool while the DMA of piece i-1 runs.
-static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes) {
+// Piece size for a transfer of `bytes`: the ring's 8 MiB, but at least four pieces per transfer
+// down to 1 MiB, so a small call (one CPI: 8 MiB of C128 echo) still overlaps its memcpy with
+// its DMA.
+static size_t piece_for(const rsp_ctx* ctx, size_t bytes) {
+    size_t p = (bytes / 4 + 4095) & ~(size_t)4095;
+    if (p < ((size_t)1 << 20)) p = (size_t)1 << 20;
+    return p < ctx->hp.piece ? p : ctx->hp.piece;
+}
+
+// `bytes` = the device-side bytes; narrow: src is complex double, narrowed to complex float on
+// the way into the pinned piece (half the PCIe bytes of MATLAB's C128 echo).
+static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes, bool narrow = false) {
     auto& h = ctx->hp;
     rsp::CopyPool& pool = host_pool(ctx);
-    for (size_t off = 0; off < bytes; off += h.piece) {
-        const size_t n = bytes - off < h.piece ? bytes - off : h.piece;
+    const size_t piece = piece_for(ctx, bytes);
+    for (size_t off = 0; off < bytes; off += piece) {
+        const size_t n = bytes - off < piece ? bytes - off : piece;
         const int r = h.ring_in;
         h.ring_in = (h.ring_in + 1) % h.kRing;
         HIP_TRY(ctx, hipEventSynchronize(h.ev_pin_in[r]));   // the slot's previous DMA is done
-        pool.copy(h.pin_in[r], (const char*)src + off, n);
+        if (narrow)
+            pool.narrow_c128((float*)h.pin_in[r], (const double*)((const char*)src + 2 * off), n / 8);
+        else
+            pool.copy(h.pin_in[r], (const char*)src + off, n);
         HIP_TRY(ctx, hipMemcpyAsync((char*)d + off, h.pin_in[r], n, hipMemcpyHostToDevice, h.s_h2d));
         HIP_TRY(ctx, hipEventRecord(h.ev_pin_in[r], h.s_h2d));
     }
@@ -1447,9 +1462,11 @@ static int d2h_pieces(rsp_ctx* ctx, const std::vector<D2HPart>& parts) {
         size_t n;
     };
     std::vector<Piece> ps;
-    for (const D2HPart& p : parts)
-        for (size_t off = 0; off < p.bytes; off += h.piece)
-            ps.push_back({(const char*)p.d + off, (char*)p.h + off, p.bytes - off < h.piece ? p.bytes - off : h.piece});
+    for (const D2HPart& p : parts) {
+        const size_t piece = piece_for(ctx, p.bytes);
+        for (size_t off = 0; off < p.bytes; off += piece)
+            ps.push_back({(const char*)p.d + off, (char*)p.h + off, p.bytes - off < piece ? p.bytes - off : piece});
+    }
     const size_t np = ps.size();
     auto issue = [&](size_t i) -> int {
         const int r = (int)(i % h.kRing);
@@ -1492,9 +1509,14 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
     if ((rc = host_pipe_init(ctx))) return rc;
     auto& h = ctx->hp;
     const int64_t Ro = ctx->p.R_out, V = ctx->V, beams = ctx->beams;
-    const size_t in_cpi = (size_t)beams * P * R * dtype_size(dtype);
+    // MATLAB's complex double is narrowed to complex float by the host copy threads (the same
+    // round-to-nearest cast the device conversion does): half the PCIe bytes
+    const bool narrow = dtype == RSP_C128;
+    const int32_t ddtype = narrow ? RSP_C64 : dtype;              // what lands on the device
+    const size_t in_cpi = (size_t)beams * P * R * dtype_size(dtype);         // caller's bytes
+    const size_t dev_cpi = (size_t)beams * P * R * dtype_size(ddtype);       // device bytes
     const size_t cells = (size_t)V * Ro;   // per CPI
-    const bool conv = !(layout == RSP_ROWMAJOR && (dtype == RSP_C64 || dtype == RSP_C32F16));
+    const bool conv = layout != RSP_ROWMAJOR;   // column-major: transposed on the device
     const bool tr = out_layout == RSP_COLMAJOR;
     const bool want_fv = cfar && flagV_out;
     int64_t K = ctx->host_chunk > 0 ? ctx->host_chunk : (int64_t)(kHostChunkBytes / in_cpi);
@@ -1502,7 +1524,7 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
     if (K > batch) K = batch;
     const int64_t nk = (batch + K - 1) / K;
     for (int i = 0; i < h.kSlots && i < nk; ++i) {
-        if ((rc = ensure(ctx, h.in[i], (size_t)K * in_cpi))) return rc;
+        if ((rc = ensure(ctx, h.in[i], (size_t)K * dev_cpi))) return rc;
         if (conv && (rc = ensure(ctx, h.canon[i], (size_t)K * beams * P * R * sizeof(float2)))) return rc;
         if ((rc = ensure(ctx, h.rdm[i], (size_t)K * cells * sizeof(float)))) return rc;
         if (cfar && (rc = ensure(ctx, h.flag[i], (size_t)K * cells))) return rc;
@@ -1521,9 +1543,9 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_in[sl], 0));
         if (k >= h.kSlots) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_out[sl], 0));   // slot's D2H done
         const void* d_echo = h.in[sl].p;
-        int32_t d_dtype = dtype;
+        int32_t d_dtype = ddtype;
         if (conv) {
-            HIP_TRY(ctx, rsp::launch_ingest(h.in[sl].p, dtype, layout, (float2*)h.canon[sl].p, n * beams, (int)P,
+            HIP_TRY(ctx, rsp::launch_ingest(h.in[sl].p, ddtype, layout, (float2*)h.canon[sl].p, n * beams, (int)P,
                                             (int)R, ctx->stream));
             d_echo = h.canon[sl].p;
             d_dtype = RSP_C64;
@@ -1563,7 +1585,8 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
         const int sl = (int)(k % h.kSlots);
         // the slot's previous chain (chunk k-2) has read its input
         if (k >= h.kSlots) HIP_TRY(ctx, hipStreamWaitEvent(h.s_h2d, h.ev_comp[sl], 0));
-        if ((rc = h2d_pieces(ctx, h.in[sl].p, (const char*)echo + (size_t)k * K * in_cpi, (size_t)chunk_n(k) * in_cpi)))
+        if ((rc = h2d_pieces(ctx, h.in[sl].p, (const char*)echo + (size_t)k * K * in_cpi, (size_t)chunk_n(k) * dev_cpi,
+                             narrow)))
             return rc;
         HIP_TRY(ctx, hipEventRecord(h.ev_in[sl], h.s_h2d));
         if ((rc = compute(k))) return rc;

@@ -1,7 +1,8 @@
 // rsp_hostpool.h -- host-side helpers of the pipelined host-buffer entry points
 // (rsp_pc_mtd_cfar / rsp_pc_mtd with MATLAB's pageable arrays): a small persistent thread pool
-// for the pageable <-> pinned staging copies.  One memcpy thread reads and writes host DRAM at
-// ~10 GB/s, well below a PCIe Gen5 x16 DMA, so each staging piece is split over the pool.
+// for the pageable <-> pinned staging copies.  One memcpy thread moves 20-30 GB/s of host DRAM,
+// 8 threads ~130 GB/s (profiles/r04/probe1/pcie_probe.txt), against ~57 GB/s of PCIe Gen5 DMA
+// per direction, so each staging piece is split over the pool.
 #pragma once
 #include <condition_variable>
 #include <cstring>
@@ -30,17 +31,32 @@ public:
     // memcpy(dst, src, bytes) split into n_ page-aligned parts; the caller runs part 0 and
     // returns when every part is done.  Small copies stay on the calling thread.
     void copy(void* dst, const void* src, size_t bytes) {
-        if (n_ == 1 || bytes < (size_t)kMinSplit) {
-            std::memcpy(dst, src, bytes);
+        char* d = (char*)dst;
+        const char* sp = (const char*)src;
+        run(bytes, 4096, [=](size_t a, size_t b) { std::memcpy(d + a, sp + a, b - a); });
+    }
+
+    // complex double -> complex float (MATLAB's C128 echo -> the chain's C64), `n` complex
+    // samples: the (float) casts round to nearest-even exactly as the GPU's v_cvt_f32_f64, so the
+    // chain sees the same samples as when it converts on the device.
+    void narrow_c128(float* dst, const double* src, size_t n) {
+        run(n, 512, [=](size_t a, size_t b) {
+            for (size_t i = 2 * a; i < 2 * b; ++i) dst[i] = (float)src[i];
+        });
+    }
+
+    // fn(begin, end) over [0, n) in n_ parts aligned to `align` elements; the caller runs part 0
+    void run(size_t n, size_t align, const std::function<void(size_t, size_t)>& fn) {
+        if (n_ == 1 || n * 8 < (size_t)kMinSplit) {
+            fn(0, n);
             return;
         }
-        size_t per = (bytes + n_ - 1) / n_;
-        per = (per + 4095) & ~(size_t)4095;
+        size_t per = (n + n_ - 1) / n_;
+        per = (per + align - 1) / align * align;
         {
             std::lock_guard<std::mutex> g(m_);
-            dst_ = (char*)dst;
-            src_ = (const char*)src;
-            bytes_ = bytes;
+            fn_ = &fn;
+            n_items_ = n;
             per_ = per;
             pending_ = n_ - 1;
             ++gen_;
@@ -55,9 +71,9 @@ private:
     static constexpr int kMinSplit = 1 << 20;
     void part(int i) {
         const size_t a = (size_t)i * per_;
-        if (a >= bytes_) return;
-        const size_t b = a + per_ < bytes_ ? a + per_ : bytes_;
-        std::memcpy(dst_ + a, src_ + a, b - a);
+        if (a >= n_items_) return;
+        const size_t b = a + per_ < n_items_ ? a + per_ : n_items_;
+        (*fn_)(a, b);
     }
     void loop(int i) {
         uint64_t seen = 0;
@@ -82,9 +98,8 @@ private:
     bool stop_ = false;
     uint64_t gen_ = 0;
     int pending_ = 0;
-    char* dst_ = nullptr;
-    const char* src_ = nullptr;
-    size_t bytes_ = 0, per_ = 0;
+    const std::function<void(size_t, size_t)>* fn_ = nullptr;
+    size_t n_items_ = 0, per_ = 0;
 };
 
 }  // namespace rsp
