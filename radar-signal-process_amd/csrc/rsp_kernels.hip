@@ -899,7 +899,7 @@ __device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t 
     // row by row: one ballot per row of the run gives the row's hit lanes, so the wave's
     // entries go out row-major -- each store instruction writes the row's hits as one
     // contiguous run (a lane-major run per lane made every store a scatter), and neighbouring
-    // entries are neighbouring columns of one row, whose 27-cell range windows overlap.  The
+    // entries are neighbouring columns of one row, whose range windows overlap.  The
     // counts are scalar (popcounts of the ballots): one LDS atomic per wave, no shuffles.
     uint32_t total = 0;
 #pragma unroll
@@ -1069,12 +1069,51 @@ __device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nw
 // The range-stage share of one MTD workgroup for the reference's window (5 reference + 7 guard
 // cells, executeCFAR.m:45-84 with Function_CFAR1D_sub_fixCells.m:34-58): its region's first
 // blockDim hits, one per thread.  The hit count and the thread's hit index are loaded before
-// the tile, the 27 RDM cells r-13 .. r+13 of the hit's row right after the tile's own loads,
+// the tile, the 17 RDM cells of the hit's row that the test reads (r-13 .. r-7, r-1 .. r+1,
+// r+7 .. r+13) right after the tile's own loads,
 // and the test + first-maximum scatter run after the tile -- the three dependent gathers hide
 // under the tile's FFT and Doppler CFAR instead of trailing the workgroup.
 struct RangeJob57 {
-    static constexpr int H = 13, NX = 2 * H + 1;
+    // the cells executeCFAR's fixCells test of r-1, r, r+1 reads (5 reference cells beyond 7 guard
+    // cells on each side): r-13 .. r-7, r-1 .. r+1, r+7 .. r+13
+    static constexpr int NX = 17;
     static constexpr int kLoads = NX;   // fetch_cells' gathers (the hook of mtd_tile)
+    static __device__ __forceinline__ constexpr int cell_off(int k) { return k < 7 ? k - 13 : (k < 10 ? k - 8 : k - 3); }
+    // the NX cells of hit column r in row `row` (range-checked: zero outside [0, R), on a
+    // zeroed row or for a lane without a hit), issued as one batch
+    static __device__ __forceinline__ void gather(float (&x)[NX], __amdgpu_buffer_rsrc_t rr, uint32_t row, int r,
+                                                  bool live, int R) {
+        const uint32_t rowoff = row * (uint32_t)R;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) {
+            const int q = r + cell_off(k);
+            const bool ok = live && q >= 0 && q < R;
+            x[k] = buf_ld_f(rr, ok ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
+        }
+    }
+    // executeCFAR.m:45-84 at hit column r: the fixCells test of r-1, r, r+1 (one-sided windows
+    // at the segment edges) and the first maximum among the passing cells, or -1
+    static __device__ __forceinline__ int test(const float (&x)[NX], int r, int slo, int shi, const CfarRArgs& c) {
+        int best = -1;
+        float bx = 0.f;
+#pragma unroll
+        for (int e = -1; e <= 1; ++e) {
+            const int q = r + e;   // left window q-12 .. q-8 = x[e+1 ..], centre x[8+e], right q+8 .. q+12
+            float sl = 0.f, sr = 0.f;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                sl += x[e + 1 + k];
+                sr += x[11 + e + k];
+            }
+            const bool lok = q - 12 >= slo, rok = q + 12 < shi;
+            const float xq = x[8 + e];
+            if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, c.method, c.Tr) && (best < 0 || xq > bx)) {
+                best = q;
+                bx = xq;
+            }
+        }
+        return best;
+    }
     uint32_t n = 0, idx = 0;
     float x[NX];
     __device__ __forceinline__ void fetch_idx(const MtdArgs& a, int rg) {
@@ -1084,7 +1123,7 @@ struct RangeJob57 {
         idx = a.prev_hits[(size_t)rg * a.prev_region + threadIdx.x];
     }
     __device__ __forceinline__ void fetch_cells(const MtdArgs& a) {
-        // Every wave of every MTD workgroup issues these 27 loads, unconditionally: a lane
+        // Every wave of every MTD workgroup issues these 17 loads, unconditionally: a lane
         // without a cell (no hit, no job) loads through the buffer range check (voffset kOob:
         // 0, no memory access).  A branch around them would leave the waits of the tile's FFT
         // (vmcnt counts in issue order) merged from two paths, so a wave with hits would wait
@@ -1096,14 +1135,7 @@ struct RangeJob57 {
         const int r = (int)(idx - row * R);
         const int v = (int)(row % V);
         const bool zrow = v >= c.cz_lo && v < c.cz_hi;
-        const auto rr = buf_rsrc(a.prev_rdm, kOob);   // job => the chunk's RDM is < kOob bytes
-        const uint32_t rowoff = row * R;
-#pragma unroll
-        for (int k = 0; k < NX; ++k) {
-            const int q = r - H + k;
-            const bool ok = mine && !zrow && q >= 0 && q < c.R;
-            x[k] = buf_ld_f(rr, ok ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
-        }
+        gather(x, buf_rsrc(a.prev_rdm, kOob), row, r, mine && !zrow, c.R);   // (job => the RDM is < kOob bytes)
     }
     __device__ __forceinline__ void finish(const MtdArgs& a) {
         if (threadIdx.x >= n) return;
@@ -1113,24 +1145,7 @@ struct RangeJob57 {
         int slo, shi;
         seg_of(r, c.nseg, c.seg_lo, c.seg_hi, slo, shi);
         if (shi <= slo) return;
-        int best = -1;
-        float bx = 0.f;
-#pragma unroll
-        for (int e = -1; e <= 1; ++e) {
-            const int q = r + e, i = H + e;   // x[i] = cell q
-            float sl = 0.f, sr = 0.f;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                sl += x[i - 12 + k];
-                sr += x[i + 8 + k];
-            }
-            const bool lok = q - 12 >= slo, rok = q + 12 < shi;
-            const float xq = x[i];
-            if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, c.method, c.Tr) && (best < 0 || xq > bx)) {
-                best = q;
-                bx = xq;
-            }
-        }
+        const int best = test(x, r, slo, shi, c);
         if (best >= 0) a.prev_flag[(size_t)row * c.R + best] = 1;
     }
 };
@@ -2006,7 +2021,7 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits_kernel(const float* __r
 // per workgroup.  A region is one MTD tile's hit list (~10-50 hits at c3-c5), so a workgroup
 // per region left most of its threads idle and took one dependent round-trip chain (count ->
 // index -> cells) per region; here the count and the lane's first index load together (the
-// index is in bounds past the count: a region holds W*P >= 256 entries), the lane's 27 cells
+// index is in bounds past the count: a region holds W*P >= 256 entries), the lane's 17 cells
 // follow as one batch of range-checked buffer loads (RangeJob57's gathers), and hits past the
 // first 64 of a region follow in further batches of 64 the same way.
 __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* __restrict__ rdm,
@@ -2017,7 +2032,7 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* _
     const int rg = (int)(blockIdx.x * (kHitThreads / 64) + threadIdx.x / 64);
     if (rg >= nregions) return;   // (wave-uniform; no barriers below)
     const int k = (int)(threadIdx.x % 64);
-    constexpr int H = RangeJob57::H, NX = RangeJob57::NX;
+    constexpr int NX = RangeJob57::NX;
     const uint32_t* list = hits + (size_t)rg * region;
     const uint32_t n = counts[rg];
     uint32_t idx = list[k];
@@ -2034,34 +2049,12 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* _
         const int v = (int)(row % V);
         const bool zrow = v >= a.cz_lo && v < a.cz_hi;
         float x[NX];
-#pragma unroll
-        for (int q = 0; q < NX; ++q) {
-            const int c = r - H + q;
-            const bool ok = mine && !zrow && c >= 0 && c < a.R;
-            x[q] = buf_ld_f(rr, ok ? (row * R + (uint32_t)c) * 4u : kOob, 0u);
-        }
+        RangeJob57::gather(x, rr, row, r, mine && !zrow, a.R);
         if (mine) {
             int slo, shi;
             seg_of(r, a.nseg, a.seg_lo, a.seg_hi, slo, shi);
             if (shi > slo) {
-                int best = -1;
-                float bx = 0.f;
-#pragma unroll
-                for (int e = -1; e <= 1; ++e) {
-                    const int q = r + e, i = H + e;   // x[i] = cell q
-                    float sl = 0.f, sr = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) {
-                        sl += x[i - 12 + j];
-                        sr += x[i + 8 + j];
-                    }
-                    const bool lok = q - 12 >= slo, rok = q + 12 < shi;
-                    const float xq = x[i];
-                    if (q >= slo && q < shi && cfar_test(xq, sl, sr, lok, rok, a.method, a.Tr) && (best < 0 || xq > bx)) {
-                        best = q;
-                        bx = xq;
-                    }
-                }
+                const int best = RangeJob57::test(x, r, slo, shi, a);
                 if (best >= 0) flag[(size_t)row * R + best] = 1;
             }
         }

@@ -136,9 +136,9 @@ class Engine:
                 flagV = np.empty(oshape, np.uint8) if want_flagV else None
             else:
                 flag, flagV = out[1], out[2]
-        for o, dt in ((rdm, np.float32), (flag, np.uint8), (flagV, np.uint8)):
-            if o is not None and (o.shape != oshape or o.dtype != dt or not o.flags.c_contiguous):
-                raise ValueError("output arrays must be C-contiguous %s of shape %s" % (dt.__name__, oshape))
+        for o, want in ((rdm, np.float32), (flag, np.uint8), (flagV, np.uint8)):
+            if o is not None and (o.shape != oshape or o.dtype != want or not o.flags.c_contiguous):
+                raise ValueError("output arrays must be C-contiguous %s of shape %s" % (want.__name__, oshape))
         rc = self.lib.rsp_pc_mtd_cfar(self.ctx, _ptr(a), dt, layout, P, self.spec.R, batch,
                                       C.byref(cp) if cp is not None else None, _ptr(rdm), out_layout,
                                       _ptr(flag), _ptr(flagV))

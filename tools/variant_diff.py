@@ -11,10 +11,11 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "gpurun_out")
+OUT = "/tmp/rsp_vdiff"   # (64 MB per plane: kept out of gpurun_out, which travels back)
 
 
 def run_one(name):
+    os.makedirs(OUT, exist_ok=True)
     sys.path.insert(0, os.path.join(ROOT, "radar-signal-process_amd"))
     import numpy as np
     import torch
