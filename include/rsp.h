@@ -193,8 +193,8 @@ int rsp_set_streams(rsp_ctx* ctx, int32_t n);
  * chunks k+1 and k-1 (two copy streams beside the context's stream); the pageable <-> pinned
  * staging runs through rings of 8 MiB pinned pieces copied by a host thread pool, so the copies
  * of one CPI also overlap their DMA.  Outputs are identical to the _dev path's. */
-/* CPIs per host chunk (0 = by size: 32 MiB of input) and host copy threads (0 = default:
- * 8 with >= 16 hardware threads). */
+/* CPIs per host chunk (0 = by size: 32 MiB of device-side input, 8 CPIs at 128 x 4096) and
+ * host copy threads (0 = default: 8 with >= 16 hardware threads). */
 int rsp_set_host_pipeline(rsp_ctx* ctx, int64_t cpis_per_chunk, int32_t copy_threads);
 
 int rsp_pc_mtd(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,

@@ -1381,7 +1381,8 @@ static int check_host_call(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_
 
 // ---- pipelined host path
 static constexpr size_t kHostPiece = 8u << 20;        // pinned piece
-static constexpr size_t kHostChunkBytes = 32u << 20;  // caller's input bytes per host chunk
+static constexpr size_t kHostChunkBytes = 32u << 20;  // device-side input bytes per host chunk
+                                                      // (c3: 8 CPIs; tools/host_probe.py)
 
 static int host_pipe_init(rsp_ctx* ctx) {
     auto& h = ctx->hp;
@@ -1519,7 +1520,7 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
     const bool conv = layout != RSP_ROWMAJOR;   // column-major: transposed on the device
     const bool tr = out_layout == RSP_COLMAJOR;
     const bool want_fv = cfar && flagV_out;
-    int64_t K = ctx->host_chunk > 0 ? ctx->host_chunk : (int64_t)(kHostChunkBytes / in_cpi);
+    int64_t K = ctx->host_chunk > 0 ? ctx->host_chunk : (int64_t)(kHostChunkBytes / dev_cpi);
     if (K < 1) K = 1;
     if (K > batch) K = batch;
     const int64_t nk = (batch + K - 1) / K;

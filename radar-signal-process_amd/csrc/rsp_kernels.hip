@@ -1162,13 +1162,16 @@ struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
 
-// MTD tile loads by LDS-DMA (dev-only -DRSP_MTD_DMA, A/B of VERDICT r3 item 1): one beam, no
-// MTI, default cache policy.  The tile's P rows of W complex columns (W*8 bytes each) go to LDS
-// as 16-byte pieces: a wave instruction covers 64/(W/2) whole rows; a lane past R_out (partial
-// right-edge tile) or a row past pin loads 0 through the range check.
+// MTD tile loads by LDS-DMA (round 4; A/B in profiles/r04/ab/: c4 +5.8 %,
+// c3 +1.5 %, c5 +0.4 %, outputs bit-identical): one beam, no MTI, default cache policy.  The
+// tile's P rows of W complex columns (W*8 bytes each) go to LDS as 16-byte pieces
+// (buffer_load_dwordx4 ... lds, no VGPR destination); a wave instruction covers 64/(W/2) whole
+// rows; a row past pin loads 0 through the range check.  The range job's gathers issue behind the
+// pieces and stay in flight across the barrier.  -DRSP_MTD_NO_DMA (dev-only) restores register
+// loads for A/B runs.
 template <int P, int BEAMS, int LA, int W>
 __host__ __device__ constexpr bool kMtdDma() {
-#ifdef RSP_MTD_DMA
+#ifndef RSP_MTD_NO_DMA
     return BEAMS == 1 && LA == 0 && W >= 2 && W <= 128 && 64 % (W / 2) == 0;
 #else
     return false;
