@@ -1084,11 +1084,11 @@ struct RangeJob57 {
     static __device__ __forceinline__ void gather(float (&x)[NX], __amdgpu_buffer_rsrc_t rr, uint32_t row, int r,
                                                   bool live, int R) {
         const uint32_t rowoff = row * (uint32_t)R;
+        const uint32_t rlive = live ? (uint32_t)R : 0u;   // q in [0, R) of a live lane: one unsigned compare
 #pragma unroll
         for (int k = 0; k < NX; ++k) {
             const int q = r + cell_off(k);
-            const bool ok = live && q >= 0 && q < R;
-            x[k] = buf_ld_f(rr, ok ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
+            x[k] = buf_ld_f(rr, (uint32_t)q < rlive ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
         }
     }
     // executeCFAR.m:45-84 at hit column r: the fixCells test of r-1, r, r+1 (one-sided windows
@@ -1322,6 +1322,10 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     const auto dfr = buf_rsrc(want_diff ? T.diff : nullptr, want_diff ? plane * 4u : 0u);
     const uint32_t vo_out = rv ? cell * 4u : kOob;
     const int srot = a.shift / G;
+    // fun_0v_pressing's zeroed rows [z_lo, z_hi) as one unsigned compare per row (and the DMX
+    // zeroSetFlagMTD band's wrap through row 0, v + P < z_hi, only when the band reaches past P)
+    const uint32_t zspan = (uint32_t)(a.z_hi - a.z_lo);
+    const bool zwrap = a.z_hi > P;
     float mg[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
@@ -1334,7 +1338,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             x += m0[m];                                                                      // |L| + |R|
         }
         // fun_0v_pressing band, or the DMX zeroSetFlagMTD band wrapping through row 0
-        if ((v >= a.z_lo && v < a.z_hi) || v + P < a.z_hi) x = 0.f;
+        if (((uint32_t)(v - a.z_lo) < zspan) | (zwrap & (v + P < a.z_hi))) x = 0.f;
         mg[m] = x;
         if constexpr (SA != 0) buf_st_fa<SA>(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
         else buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
@@ -1344,12 +1348,13 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     __syncthreads();  // the FFT exchange slots are free from here on
     float* mag = REF > 0 ? reinterpret_cast<float*>(smem) + c * C::MS2 + C::SPAD
                          : reinterpret_cast<float*>(smem) + c * C::MS;
+    const uint32_t czspan = a.cv.cz_hi > a.cv.cz_lo ? (uint32_t)(a.cv.cz_hi - a.cv.cz_lo) : 0u;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         int mm = m + srot;
         if (mm >= E) mm -= E;
         const int v = g + G * mm;
-        mag[v] = (v >= a.cv.cz_lo && v < a.cv.cz_hi) ? 0.f : mg[m];   // main_cfar.m:90-91
+        mag[v] = (uint32_t)(v - a.cv.cz_lo) < czspan ? 0.f : mg[m];   // main_cfar.m:90-91
     }
     __syncthreads();
 
