@@ -879,39 +879,44 @@ struct DopplerOut {
 // flagV / flag bytes where requested (uniform branches, once per run), and the hits appended to
 // the workgroup's list.  Hits are sparse, so the append path is entered only by waves that
 // have one: one ballot over the masks, then per row one ballot and one LDS atomic per wave.
-template <int N>
-__device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t mask) {
+template <int N, typename Hit>
+__device__ __forceinline__ void doppler_emit(const DopplerOut& o, bool anyhit, const Hit& hit) {
     if (o.want_fv) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) buf_st_u8((mask >> i) & 1u, o.fv, o.vo, (uint32_t)i * o.R);
+        for (int i = 0; i < N; ++i) buf_st_u8(hit(i) ? 1u : 0u, o.fv, o.vo, (uint32_t)i * o.R);
     }
     if (!o.fused) return;
     if (!o.rflag) {   // flag = flagV (executeCFAR.m:91)
 #pragma unroll
-        for (int i = 0; i < N; ++i) buf_st_u8((mask >> i) & 1u, o.fl, o.vo, (uint32_t)i * o.R);
+        for (int i = 0; i < N; ++i) buf_st_u8(hit(i) ? 1u : 0u, o.fl, o.vo, (uint32_t)i * o.R);
         return;
     }
     if (o.zero_bg) {   // zero background (here, or pre-zeroed); the range stage sets the detections
 #pragma unroll
         for (int i = 0; i < N; ++i) buf_st_u8(0, o.fl, o.vo, (uint32_t)i * o.R);
     }
-    if (__ballot(mask != 0u) == 0) return;   // the common case: no hit in the wave's rows
+    if (__ballot(anyhit) == 0) return;   // the common case: no hit in the wave's rows
     // row by row: one ballot per row of the run gives the row's hit lanes, so the wave's
     // entries go out row-major -- each store instruction writes the row's hits as one
     // contiguous run (a lane-major run per lane made every store a scatter), and neighbouring
     // entries are neighbouring columns of one row, whose range windows overlap.  The
-    // counts are scalar (popcounts of the ballots): one LDS atomic per wave, no shuffles.
+    // counts are scalar (popcounts of the ballots, each taken once): one LDS atomic per wave,
+    // its result broadcast by readfirstlane (no shuffle through LDS).
+    uint64_t bal[N];
     uint32_t total = 0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) total += (uint32_t)__popcll(__ballot((mask >> i) & 1u));
+    for (int i = 0; i < N; ++i) {
+        bal[i] = __ballot(hit(i));
+        total += (uint32_t)__popcll(bal[i]);
+    }
     uint32_t base = 0;
     if (__lane_id() == 0) base = atomicAdd(o.lds_count, total);
-    base = __shfl(base, 0);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const uint64_t b = __ballot((mask >> i) & 1u);
+        const uint64_t b = bal[i];
         if (b == 0) continue;   // (wave-uniform)
-        if ((mask >> i) & 1u) {
+        if (hit(i)) {
             const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
             uint32_t* dst = o.hits + base + below;
             if (o.coherent) st_u32_sc1(dst, o.cell0 + (uint32_t)i * o.R);
@@ -919,6 +924,12 @@ __device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t 
         }
         base += (uint32_t)__popcll(b);
     }
+}
+
+// the same for a row bit mask (bit i = row v0+i is a hit)
+template <int N>
+__device__ __forceinline__ void doppler_emit_mask(const DopplerOut& o, uint32_t mask) {
+    doppler_emit<N>(o, mask != 0u, [&](int i) { return ((mask >> i) & 1u) != 0u; });
 }
 
 template <int N>
@@ -960,8 +971,9 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
     const int kr = cv.hi - cv.save - 1 - REF - v0; // ... and a right window iff i <= kr
     const int b0 = cv.lo - v0, b1 = cv.hi - v0;    // tested rows: b0 <= i < b1
     const bool go = cv.method == 0;
-    static_assert(E <= 32, "row mask");
-    uint32_t mask = 0;
+    // per-row hit predicates (lane masks, not a packed bit mask: each row's ballot is then the
+    // compare's own result, with no bit packing and extraction around it)
+    bool h[E];
     if (kl <= 0 && kr >= E - 1 && b0 <= 0 && b1 >= E && go) {
         // the common case: every row of the run is tested and has both windows (GO): the same
         // sums and compare-select as below, without the per-row window and band selects
@@ -974,9 +986,8 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
                 sr += Rw[i + q];
             }
             const float th = (sl > sr ? sl : sr) * cv.Tr;
-            mask |= (m[i] >= th ? 1u : 0u) << i;
+            h[i] = col_on & (m[i] >= th);
         }
-        if (!col_on) mask = 0u;
     } else {
 #pragma unroll
         for (int i = 0; i < E; ++i) {
@@ -990,12 +1001,14 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
             const float x = lok ? sl : sr, y = rok ? sr : sl;   // one-sided fallback (:30-39)
             // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
             const float th = (go ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
-            const bool hit = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
-            mask |= (hit ? 1u : 0u) << i;
+            h[i] = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
         }
     }
-    // (outside the divergent branches: the emission's ballots and shuffles need every lane)
-    doppler_emit_mask<E>(o, mask);
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < E; ++i) any |= h[i];
+    // (outside the divergent branches: the emission's ballots need every lane)
+    doppler_emit<E>(o, any, [&](int i) { return h[i]; });
 }
 
 // Threads first, first + step, ... evaluate the hits of region rg: REF/SAVE > 0 compile-time
@@ -1153,12 +1166,15 @@ struct RangeJob57 {
 struct RangeHook {   // mtd_tile's after_loads(): the range job's gathers
     RangeJob57& rj;
     const MtdArgs& a;
+    bool job;           // workgroup-uniform: this workgroup has a range job
     static constexpr int kLoads = RangeJob57::kLoads;
+    __device__ __forceinline__ bool active() const { return job; }
     __device__ __forceinline__ void operator()() const { rj.fetch_cells(a); }
 };
 
 struct NoHook {
     static constexpr int kLoads = 0;   // vector-memory operations operator() issues
+    __device__ __forceinline__ bool active() const { return false; }
     __device__ __forceinline__ void operator()() const {}
 };
 
@@ -1269,8 +1285,12 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             // (a compiler barrier: the range gathers below must issue after every DMA piece, or
             // the counted vmcnt would not cover the pieces -- hipcc interleaved them otherwise)
             asm volatile("" ::: "memory");
-            after_loads();
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Hook::kLoads) : "memory");
+            if (after_loads.active()) {   // (workgroup-uniform) a workgroup without a range job
+                after_loads();            // skips the gathers and their address arithmetic
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Hook::kLoads) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __builtin_amdgcn_s_barrier();
             const float2* l = reinterpret_cast<const float2*>(smem);
 #pragma unroll
@@ -1444,7 +1464,7 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     RSP_STAMP(1, 0, false);
     RSP_STAMP_RT(1, 8);
     if (job) rj.fetch_idx(a, (int)wg);
-    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a});
+    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a, job});
     RSP_STAMP(1, 5, false);
     rj.finish(a);
     RSP_STAMP(1, 6, false);
