@@ -942,65 +942,80 @@ __device__ __forceinline__ void doppler_flags(const float* mag, const float* sum
     doppler_emit_mask<N>(o, mask);
 }
 
-// Doppler CFAR with a compile-time reference window REF (the reference's default 5; the
-// guard `save`, the method and the row band stay runtime).  A thread owns a run of E rows of
-// one range column: it reads its rows, their left windows and their right windows from the
-// padded magnitude column once (three bases, immediate offsets) and forms all 2E window sums
-// in registers -- no sums array, no second barrier, and the LDS footprint stays inside the
-// FFT exchange area (one more resident workgroup per CU than a sums column allows).
+// Doppler CFAR with the reference's window compiled in (REF = 5 reference and SAVE = 7 guard
+// cells, main_cfar.m:40-58; other windows take the runtime path; the method and the row band
+// stay runtime).  A thread owns a run of E rows of one range column: it reads its rows and the
+// (left, right) window cells of every row as pairs from the padded magnitude column -- the two
+// cells of a pair lie 2 SAVE + REF + 1 apart, one ds_read2 into a register pair -- and forms each
+// row's two window sums together with packed adds (each sum still the left-to-right add of its
+// REF cells, mean()'s order), in registers: no sums array, no second barrier, and the LDS
+// footprint stays inside the FFT exchange area.
 template <int P, int REF, int BEAMS>
 __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarVArgs& cv, bool col_on, int v0,
                                                    const DopplerOut& o) {
+    static_assert(REF == 5, "the compiled-in window is the reference's (5 reference, 7 guard cells)");
+    constexpr int SAVE = 7;
     // mag: this column's magnitudes, mag[v] for v in [-SPAD, P + SPAD) (pad cells unused:
     // every row in [lo, hi) has at least one window inside the column, the other is selected
-    // away).  The left window of row v0+i starts at v0+i-save-REF, the right one at
-    // v0+i+save+1; each sum is the direct left-to-right add of its REF cells (mean()'s order).
-    constexpr int E = MtdCfg<P, BEAMS>::E, NL = E + REF - 1;
-    const float* bl = mag + v0 - cv.save - REF;
-    const float* br = mag + v0 + cv.save + 1;
-    const float* bm = mag + v0;
-    float L[NL], Rw[NL], m[E];
+    // away).  The left window of row v0+i starts at v0+i-SAVE-REF, the right one at
+    // v0+i+SAVE+1.
+    constexpr int E = MtdCfg<P, BEAMS>::E, NL = E + REF - 1, DLR = 2 * SAVE + REF + 1;
+    const float* bl = mag + v0 - SAVE - REF;
+    v2f lr[NL];   // (left cell, right cell) of window position i: bl[i], bl[i + DLR]
+    float m[E];   // the cells under test, bl[SAVE + REF + i]: inside the pairs' span
+    if constexpr (NL == 20 && DLR == 20) {
+        // one asm block: 20 ds_read2_b32 straight into the pairs (hipcc merges neighbouring
+        // cells instead and spends ~40 v_mov re-pairing them), and the wait on them
+        const uint32_t ad = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)bl;
+#define RSP_PAIR_LD(i, j) "ds_read2_b32 %" #i ", %20 offset0:" #i " offset1:" #j "\n\t"
+        asm volatile(RSP_PAIR_LD(0, 20) RSP_PAIR_LD(1, 21) RSP_PAIR_LD(2, 22) RSP_PAIR_LD(3, 23) RSP_PAIR_LD(4, 24)
+                     RSP_PAIR_LD(5, 25) RSP_PAIR_LD(6, 26) RSP_PAIR_LD(7, 27) RSP_PAIR_LD(8, 28) RSP_PAIR_LD(9, 29)
+                     RSP_PAIR_LD(10, 30) RSP_PAIR_LD(11, 31) RSP_PAIR_LD(12, 32) RSP_PAIR_LD(13, 33)
+                     RSP_PAIR_LD(14, 34) RSP_PAIR_LD(15, 35) RSP_PAIR_LD(16, 36) RSP_PAIR_LD(17, 37)
+                     RSP_PAIR_LD(18, 38) RSP_PAIR_LD(19, 39) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(lr[0]), "=&v"(lr[1]), "=&v"(lr[2]), "=&v"(lr[3]), "=&v"(lr[4]), "=&v"(lr[5]), "=&v"(lr[6]),
+                       "=&v"(lr[7]), "=&v"(lr[8]), "=&v"(lr[9]), "=&v"(lr[10]), "=&v"(lr[11]), "=&v"(lr[12]),
+                       "=&v"(lr[13]), "=&v"(lr[14]), "=&v"(lr[15]), "=&v"(lr[16]), "=&v"(lr[17]), "=&v"(lr[18]),
+                       "=&v"(lr[19])
+                     : "v"(ad)
+                     : "memory");
+#undef RSP_PAIR_LD
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        L[i] = bl[i];
-        Rw[i] = br[i];
+        for (int i = 0; i < E; ++i) m[i] = SAVE + REF + i < NL ? lr[SAVE + REF + i].x : lr[SAVE + REF + i - DLR].y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) lr[i] = (v2f){bl[i], bl[i + DLR]};
+#pragma unroll
+        for (int i = 0; i < E; ++i) m[i] = bl[SAVE + REF + i];
     }
-#pragma unroll
-    for (int i = 0; i < E; ++i) m[i] = bm[i];
-    const int kl = cv.lo + cv.save + REF - v0;     // row v0+i has a left window iff i >= kl
-    const int kr = cv.hi - cv.save - 1 - REF - v0; // ... and a right window iff i <= kr
-    const int b0 = cv.lo - v0, b1 = cv.hi - v0;    // tested rows: b0 <= i < b1
+    const int kl = cv.lo + SAVE + REF - v0;     // row v0+i has a left window iff i >= kl
+    const int kr = cv.hi - SAVE - 1 - REF - v0; // ... and a right window iff i <= kr
+    const int b0 = cv.lo - v0, b1 = cv.hi - v0; // tested rows: b0 <= i < b1
     const bool go = cv.method == 0;
     // per-row hit predicates (lane masks, not a packed bit mask: each row's ballot is then the
     // compare's own result, with no bit packing and extraction around it)
     bool h[E];
     if (kl <= 0 && kr >= E - 1 && b0 <= 0 && b1 >= E && go) {
         // the common case: every row of the run is tested and has both windows (GO): the same
-        // sums and compare-select as below, without the per-row window and band selects
+        // sums, the greater of the two (magnitude sums are never NaN or -0, so max is the
+        // compare-select), without the per-row window and band selects
 #pragma unroll
         for (int i = 0; i < E; ++i) {
-            float sl = L[i], sr = Rw[i];
+            v2f sw = lr[i];
 #pragma unroll
-            for (int q = 1; q < REF; ++q) {
-                sl += L[i + q];
-                sr += Rw[i + q];
-            }
-            const float th = (sl > sr ? sl : sr) * cv.Tr;
-            h[i] = col_on & (m[i] >= th);
+            for (int q = 1; q < REF; ++q) sw += lr[i + q];
+            h[i] = col_on & (m[i] >= __builtin_fmaxf(sw.x, sw.y) * cv.Tr);
         }
     } else {
 #pragma unroll
         for (int i = 0; i < E; ++i) {
-            float sl = L[i], sr = Rw[i];
+            v2f sw = lr[i];
 #pragma unroll
-            for (int q = 1; q < REF; ++q) {
-                sl += L[i + q];
-                sr += Rw[i + q];
-            }
+            for (int q = 1; q < REF; ++q) sw += lr[i + q];
+            const float sl = sw.x, sr = sw.y;
             const bool lok = i >= kl, rok = i <= kr;
             const float x = lok ? sl : sr, y = rok ? sr : sl;   // one-sided fallback (:30-39)
-            // magnitude sums are never NaN, so a compare-select is max/min (fmaxf would canonicalise)
-            const float th = (go ? (x > y ? x : y) : (x < y ? x : y)) * cv.Tr;
+            const float th = (go ? __builtin_fmaxf(x, y) : __builtin_fminf(x, y)) * cv.Tr;
             h[i] = col_on & (i >= b0) & (i < b1) & (m[i] >= th);
         }
     }
@@ -1009,6 +1024,15 @@ __device__ __forceinline__ void doppler_cfar_fixed(const float* mag, const CfarV
     for (int i = 0; i < E; ++i) any |= h[i];
     // (outside the divergent branches: the emission's ballots need every lane)
     doppler_emit<E>(o, any, [&](int i) { return h[i]; });
+}
+
+// The run of Doppler rows a CFAR thread takes: runs 0 and G-1 (the only ones near the column's
+// ends with the reference's full row band, whose windows need the one-sided selects) go to the
+// first wave's threads, so one wave of the workgroup runs the edge path instead of two.
+template <int G, int W>
+__device__ __forceinline__ int cfar_run(int g) {
+    if constexpr (64 % W == 0 && 64 / W >= 2 && G > 2) return g == 0 ? 0 : (g == 1 ? G - 1 : g - 1);
+    else return g;
 }
 
 // Threads first, first + step, ... evaluate the hits of region rg: REF/SAVE > 0 compile-time
@@ -1237,6 +1261,17 @@ struct MtdTile {
     int bx;                // tile index along range
 };
 
+// fn(mm) for the thread's rows g + G*mm (mm < E) inside [lo, hi) (G a power of two; the
+// arithmetic shift floors, so (x + G - 1) >> log2(G) is ceil(x / G) for negative x too)
+template <int G, int E, typename F>
+__device__ __forceinline__ void own_rows(int g, int lo, int hi, const F& fn) {
+    constexpr int LG = __builtin_ctz(G);
+    static_assert((G & (G - 1)) == 0, "G is a power of two");
+    const int a0 = max(0, (lo - g + G - 1) >> LG), b0 = min(E, (hi - g + G - 1) >> LG);
+#pragma clang loop unroll(disable) vectorize(disable)
+    for (int mm = a0; mm < b0; ++mm) fn(mm);
+}
+
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
 // after_loads(): called once the tile's first-beam loads are issued (RangeJob57 gathers).
@@ -1342,43 +1377,52 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     const auto dfr = buf_rsrc(want_diff ? T.diff : nullptr, want_diff ? plane * 4u : 0u);
     const uint32_t vo_out = rv ? cell * 4u : kOob;
     const int srot = a.shift / G;
-    // fun_0v_pressing's zeroed rows [z_lo, z_hi) as one unsigned compare per row (and the DMX
-    // zeroSetFlagMTD band's wrap through row 0, v + P < z_hi, only when the band reaches past P)
-    const uint32_t zspan = (uint32_t)(a.z_hi - a.z_lo);
-    const bool zwrap = a.z_hi > P;
     float mg[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         int mm = m + srot;                // fftshift: bin g + G*m -> row g + G*mm
         if (mm >= E) mm -= E;
-        const int v = g + G * mm;
         float x = __builtin_amdgcn_sqrtf(fmaf(u[m].x, u[m].x, u[m].y * u[m].y));
         if constexpr (BEAMS == 2) {
             if (want_diff) buf_st_f(x - m0[m], dfr, vo_out, (uint32_t)(G * mm) * R * 4u);   // |R| - |L|
             x += m0[m];                                                                      // |L| + |R|
         }
-        // fun_0v_pressing band, or the DMX zeroSetFlagMTD band wrapping through row 0
-        if (((uint32_t)(v - a.z_lo) < zspan) | (zwrap & (v + P < a.z_hi))) x = 0.f;
         mg[m] = x;
         if constexpr (SA != 0) buf_st_fa<SA>(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
         else buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
+    // fun_0v_pressing's zeroed rows [z_lo, z_hi) (the DMX zeroSetFlagMTD band wraps through row
+    // 0: rows [0, z_hi - P) too), as a second store of 0 to the few of the thread's rows inside
+    // the band -- the same thread's later store to the same address wins -- instead of a
+    // compare-select on every row (one or two rows per thread; 4 VALU per row saved)
+    const int zw = a.z_hi > P ? a.z_hi - P : 0;
+    auto zero_rdm = [&](int mm) {   // (mm is per lane: the row offset goes in the VGPR offset)
+        const uint32_t vz = rv ? (cell + (uint32_t)(G * mm) * R) * 4u : kOob;
+        if constexpr (SA != 0) buf_st_fa<SA>(0.f, dst, vz, 0u);
+        else buf_st_f_stream(0.f, dst, vz, 0u);
+    };
+    own_rows<G, E>(g, a.z_lo, a.z_hi, zero_rdm);
+    own_rows<G, E>(g, 0, zw, zero_rdm);
     RSP_STAMP(1, 3, false);
     if (!a.cv.enabled) return;
     __syncthreads();  // the FFT exchange slots are free from here on
     float* mag = REF > 0 ? reinterpret_cast<float*>(smem) + c * C::MS2 + C::SPAD
                          : reinterpret_cast<float*>(smem) + c * C::MS;
-    const uint32_t czspan = a.cv.cz_hi > a.cv.cz_lo ? (uint32_t)(a.cv.cz_hi - a.cv.cz_lo) : 0u;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         int mm = m + srot;
         if (mm >= E) mm -= E;
-        const int v = g + G * mm;
-        mag[v] = (uint32_t)(v - a.cv.cz_lo) < czspan ? 0.f : mg[m];   // main_cfar.m:90-91
+        mag[g + G * mm] = mg[m];
     }
+    // the CFAR input's zero rows (main_cfar.m:90-91) and the RDM's band, by the same second
+    // write of 0 (LDS writes of one thread land in order)
+    auto zero_mag = [&](int mm) { mag[g + G * mm] = 0.f; };
+    own_rows<G, E>(g, a.z_lo, a.z_hi, zero_mag);
+    own_rows<G, E>(g, 0, zw, zero_mag);
+    own_rows<G, E>(g, a.cv.cz_lo, a.cv.cz_hi, zero_mag);
     __syncthreads();
 
-    const int v0 = g * E;   // this thread's run of Doppler rows
+    const int v0 = cfar_run<G, W>(g) * E;   // this thread's run of Doppler rows
     const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
     DopplerOut o;
     o.want_fv = T.flagV != nullptr;
@@ -1626,7 +1670,7 @@ static hipError_t launch_mtd_p(const float2* pc, float* rdm, uint8_t* flagV, int
     if (a.cv.enabled && a.cv.save + a.cv.ref + 2 > C::SPAD) return hipErrorInvalidValue;
     if ((uint64_t)P * a.R_out * 8 >= (uint64_t)kOob) return hipErrorInvalidValue;
     if (a.pin < 1 || a.pin > P || a.beams != BEAMS) return hipErrorInvalidValue;
-    if (a.cv.enabled && a.cv.ref == 5) return launch_mtd_pr<P, 5, BEAMS>(pc, rdm, flagV, ncpi, a, s);
+    if (a.cv.enabled && a.cv.ref == 5 && a.cv.save == 7) return launch_mtd_pr<P, 5, BEAMS>(pc, rdm, flagV, ncpi, a, s);
     return launch_mtd_pr<P, 0, BEAMS>(pc, rdm, flagV, ncpi, a, s);
 }
 
