@@ -172,11 +172,12 @@ def test_legacy_native_chain_and_kaiser_pin(torch_cuda):
 
 @pytest.mark.parametrize("methodV,methodR,ref_n,guard,P,R", [(1, 1, 5, 7, 128, 4096), (0, 0, 3, 2, 128, 4096),
                                                             (1, 0, 8, 4, 64, 1024), (0, 1, 5, 7, 64, 1024),
-                                                            (1, 1, 3, 2, 256, 8192)])
+                                                            (1, 1, 3, 2, 256, 8192), (0, 0, 5, 4, 128, 4096)])
 def test_chain_cfar_variants(torch_cuda, methodV, methodR, ref_n, guard, P, R):
     """The fused hot path (Doppler CFAR in the MTD kernel, range stage on its hit list) with
     SO (method 1) and reference / guard windows other than the default 5 / 7 -- the runtime-
-    window MTD kernel and the generic hit-region range stage -- against the oracle."""
+    window MTD kernel (also for 5 reference cells with a guard other than 7: the compiled-in
+    window is 5 + 7 only) and the generic hit-region range stage -- against the oracle."""
     torch = torch_cuda
     import dataclasses
     from rsp import presets, synth
