@@ -67,6 +67,9 @@ def parse():
                          "host echo as MATLAB holds it, RDM + flags back to host)")
     ap.add_argument("--host-batch", type=int, default=1,
                     help="--host-path: CPIs per host call besides 32 (MATLAB calls one CPI per call)")
+    ap.add_argument("--ingest-mix", action="store_true",
+                    help="--config ingest: frames whose PRTs cycle through payload types 1 (DDC), 0 (ADC) and 3 "
+                         "(FrameDataRead_xzr.m:57-198), 16 beams, instead of all-DDC capture frames")
     ap.add_argument("--prefilter", action="store_true",
                     help="fused iSTC (a synthetic stc curve) + MTI lag 30 in the chain (rsp_set_prefilter)")
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
@@ -251,16 +254,26 @@ def bench_ingest(args, world, rank, local, dev, dist):
     resident in HBM; each rank decodes its own frames (no collective)."""
     import torch
     sys.path[:0] = [os.path.join(ROOT, "tests", "golden")]
-    from make_golden_ingest import synth_frame   # the synthetic record writer (test data only)
+    from make_golden_ingest import synth_frame, synth_mixed_frame   # synthetic record writers (test data only)
     from rsp import ingest, shard
     B = args.batch
     lo, _ = shard.weak_shard(B, rank)
-    _, dbf, _, cfg, rec = synth_frame(args.P, args.R, 16, 13, seed=3000 + lo)
+    if args.ingest_mix:
+        # PRT p carries payload type (1, 0, 3)[p % 3]: DDC, ADC (its matrix passes the :171 size
+        # check only with channel_num == beam_num, hence 16 beams) and a type without a decode
+        # case (a zero row).  Every PRT is valid, so the frame decodes to its last row.  (The
+        # 24-bit DBF branch never passes the size check with 16 channels: the reference marks
+        # it unfinished.)
+        NB = 16
+        dbf, cfg, rec = synth_mixed_frame([(1, 0, 3)[p % 3] for p in range(args.P)], args.R, 16, NB, seed=3000 + lo)
+    else:
+        NB = 13
+        _, dbf, _, cfg, rec = synth_frame(args.P, args.R, 16, NB, seed=3000 + lo)
     ing = ingest.Ingest(local)
     d_rec = torch.frombuffer(bytearray(rec), dtype=torch.uint8).to(dev)
     frames = d_rec.repeat(B)                          # B distinct frame slots of identical records
     d_dbf = ing.dbf_device(dbf)
-    out = torch.empty((B, 13, args.P, args.R), dtype=torch.complex64, device=dev)
+    out = torch.empty((B, NB, args.P, args.R), dtype=torch.complex64, device=dev)
     stream = torch.cuda.current_stream(dev)
     nb = len(rec)
 
@@ -303,7 +316,7 @@ def bench_ingest(args, world, rank, local, dev, dist):
                "sample": "%d v2 capture frames in %.1f s: fp64 numpy restatement of FrameDataRead_xzr.m "
                          "(record parse + DDC decode + DBF), BLAS limited to 1 thread" % (done, el)}
     if rank == 0:
-        unit_bytes = nb + 13 * args.P * args.R * 8                 # records read + beams written
+        unit_bytes = nb + NB * args.P * args.R * 8                 # records read + beams written
         per_frame_s = gpu_ms / 1e3 / (args.steps * B)
         ach = unit_bytes / per_frame_s / 1e9
         print(json.dumps({
@@ -314,7 +327,8 @@ def bench_ingest(args, world, rank, local, dev, dist):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16 in, f32",
             "data": "synthetic PRT records (oracle/ingest_ref.prt_record format, seeded int16 I/Q)",
             "config": {"workload": "ingest: %d frames per GPU per step, records resident in HBM" % B,
-                       "prt": args.P, "samples": args.R, "channels": 16, "beams": 13,
+                       "payload": "mixed PRTs: DDC / ADC / type 3 (no decode case)" if args.ingest_mix else "DDC (type 1)",
+                       "prt": args.P, "samples": args.R, "channels": 16, "beams": NB,
                        "parallelism": "frame-sharded x%d, no collective" % world},
             "roofline": {"bound": "hbm", "kernel": "ingest_decode_kernel", "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),

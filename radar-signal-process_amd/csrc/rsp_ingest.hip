@@ -164,6 +164,16 @@ __global__ __launch_bounds__(256) void ingest_decode_kernel(const uint8_t* __res
                                                              const int32_t* __restrict__ status) {
     const int p = blockIdx.y;
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    // generic shapes: the DBF matrix staged in LDS once per block (the host passes its size as
+    // dynamic LDS when it fits, else 0): per beam the channel sums then read their coefficients
+    // as LDS broadcasts, where scalar loads behind each beam's vector stores cost a vmcnt(0) drain
+    extern __shared__ float2 s_dbf[];
+    constexpr int kChMax = 32;   // channels a thread holds in registers on that path
+    const bool staged = CH == 0 && a.dbf_lds != 0;
+    if (staged) {
+        for (int i = threadIdx.x; i < a.beam_num * a.channel_num; i += blockDim.x) s_dbf[i] = dbf[i];
+        __syncthreads();
+    }
     const int stop = status[a.prt_num];
     if (servo && p >= stop && blockIdx.x == 0 && threadIdx.x == 0) servo[p] = 0;
     if (s >= a.point_prt) return;
@@ -233,6 +243,28 @@ __global__ __launch_bounds__(256) void ingest_decode_kernel(const uint8_t* __res
         }
 #pragma unroll
         for (int b = 0; b < NB; ++b) out[(size_t)b * a.beam_stride + o] = acc[b];
+    } else if (staged && ch <= kChMax) {   // the sample's channels loaded once, in registers
+        float2 x[kChMax];
+#pragma unroll
+        for (int c = 0; c < kChMax; ++c) {
+            if (c < ch) {   // (uniform)
+                const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(pr, (uint32_t)(s * ch + c) * 4u, 0u, 0);
+                x[c] = make_float2((float)(int16_t)(w & 0xffff), (float)(int16_t)(w >> 16));
+            }
+        }
+        for (int b = 0; b < a.beam_num; ++b) {
+            const float2* cb = s_dbf + b * ch;
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int c = 0; c < kChMax; ++c) {
+                if (c < ch) {   // (uniform; the same sums in the same order as below)
+                    const float2 cw = cb[c];
+                    acc.x = fmaf(x[c].x, cw.x, fmaf(-x[c].y, cw.y, acc.x));
+                    acc.y = fmaf(x[c].x, cw.y, fmaf(x[c].y, cw.x, acc.y));
+                }
+            }
+            out[(size_t)b * a.beam_stride + o] = acc;
+        }
     } else {
         for (int b = 0; b < a.beam_num; ++b) {
             const float2* cb = dbf + (size_t)b * ch;
@@ -258,8 +290,13 @@ hipError_t launch_ingest(const uint8_t* stream, int64_t nbytes, const IngestArgs
     const dim3 grid((unsigned)((a.point_prt + 255) / 256), (unsigned)a.prt_num);
     if (a.channel_num == 16 && a.beam_num == 13)   // the v2 capture (bin_to_mat_xzr.m:39-40)
         hipLaunchKernelGGL((ingest_decode_kernel<16, 13>), grid, dim3(256), 0, s, stream, a, dbf, out, servo, status);
-    else
-        hipLaunchKernelGGL((ingest_decode_kernel<0, 0>), grid, dim3(256), 0, s, stream, a, dbf, out, servo, status);
+    else {
+        IngestArgs g = a;
+        const size_t lds = (size_t)a.beam_num * (size_t)a.channel_num * sizeof(float2);
+        g.dbf_lds = lds <= 32768 ? 1 : 0;   // (within the default dynamic-LDS limit)
+        hipLaunchKernelGGL((ingest_decode_kernel<0, 0>), grid, dim3(256), g.dbf_lds ? lds : 0, s, stream, g, dbf, out,
+                           servo, status);
+    }
     return hipGetLastError();
 }
 

@@ -173,6 +173,7 @@ struct IngestArgs {
     int ddc_only;            // rsp_ingest_ddc_dev: records sized by the params, other types refused
     int64_t* offs;           // [prt_num] record offsets in the stream (check -> decode kernel)
     int32_t* types;          // [prt_num] data types of the decoded records
+    int dbf_lds;             // (launch_ingest) generic-shape decode: the DBF matrix staged in LDS
 };
 hipError_t launch_ingest(const uint8_t* stream, int64_t nbytes, const IngestArgs& a, const float2* dbf,
                          float2* out, uint16_t* servo, int32_t* status, hipStream_t s);
