@@ -488,6 +488,14 @@ __device__ __forceinline__ void tw_preload(float2 (&w)[NW], int t, const float2*
 // fft_reg with the twiddles of every pass already in registers (w from tw_preload)
 // Exchange synchronisation: the workgroup barrier, or (WS: the transform belongs to one wave)
 // a wave-scope fence -- a wave's LDS operations are performed in issue order.
+// Workgroup barrier for an LDS hand-off: this wave's LDS operations complete, then s_barrier.
+// __syncthreads() is a workgroup-scope release/acquire fence around the barrier, and once a
+// kernel has issued an LDS-DMA load (the MTD tile) hipcc makes every such fence wait vmcnt(0) --
+// for every global load and store the wave has in flight, e.g. the range job's gathers or the
+// RDM stores -- although only LDS changes hands here.  (The "memory" clobber keeps hipcc from
+// moving memory accesses across it.)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <bool WS>
 __device__ __forceinline__ void xsync() {
     if constexpr (WS) {
@@ -495,7 +503,7 @@ __device__ __forceinline__ void xsync() {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     } else {
-        __syncthreads();
+        lds_barrier();
     }
 }
 

@@ -1187,18 +1187,16 @@ struct RangeJob57 {
     }
 };
 
-struct RangeHook {   // mtd_tile's after_loads(): the range job's gathers
+struct RangeHook {   // mtd_tile's after_loads(): the range job's gathers (a workgroup without a
+                     // job, rj.n == 0, issues them with every lane out of range)
     RangeJob57& rj;
     const MtdArgs& a;
-    bool job;           // workgroup-uniform: this workgroup has a range job
     static constexpr int kLoads = RangeJob57::kLoads;
-    __device__ __forceinline__ bool active() const { return job; }
     __device__ __forceinline__ void operator()() const { rj.fetch_cells(a); }
 };
 
 struct NoHook {
     static constexpr int kLoads = 0;   // vector-memory operations operator() issues
-    __device__ __forceinline__ bool active() const { return false; }
     __device__ __forceinline__ void operator()() const {}
 };
 
@@ -1320,12 +1318,18 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             // (a compiler barrier: the range gathers below must issue after every DMA piece, or
             // the counted vmcnt would not cover the pieces -- hipcc interleaved them otherwise)
             asm volatile("" ::: "memory");
-            if (after_loads.active()) {   // (workgroup-uniform) a workgroup without a range job
-                after_loads();            // skips the gathers and their address arithmetic
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Hook::kLoads) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            // (one path per kernel instance -- the range job is a template choice, not a runtime
+            // branch: where a job / no-job branch merged, hipcc's waitcnt pass, which cannot read
+            // an asm wait, counted from the no-job side and made the window multiply wait for
+            // most gathers).  The weights and twiddles are older than the gathers, so the wait
+            // covers them; redefined behind it, no later use of them waits for the gathers, which
+            // stay in flight through the FFT and the Doppler CFAR (lds_barrier).
+            after_loads();
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Hook::kLoads) : "memory");
+#pragma unroll
+            for (int m = 0; m < E; ++m) asm volatile("" : "+v"(wv[m]));
+#pragma unroll
+            for (int i = 0; i < NW; ++i) asm volatile("" : "+v"(tw[i]));
             __builtin_amdgcn_s_barrier();
             const float2* l = reinterpret_cast<const float2*>(smem);
 #pragma unroll
@@ -1405,7 +1409,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     own_rows<G, E>(g, 0, zw, zero_rdm);
     RSP_STAMP(1, 3, false);
     if (!a.cv.enabled) return;
-    __syncthreads();  // the FFT exchange slots are free from here on
+    lds_barrier();  // the FFT exchange slots are free from here on
     float* mag = REF > 0 ? reinterpret_cast<float*>(smem) + c * C::MS2 + C::SPAD
                          : reinterpret_cast<float*>(smem) + c * C::MS;
 #pragma unroll
@@ -1420,7 +1424,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     own_rows<G, E>(g, a.z_lo, a.z_hi, zero_mag);
     own_rows<G, E>(g, 0, zw, zero_mag);
     own_rows<G, E>(g, a.cv.cz_lo, a.cv.cz_hi, zero_mag);
-    __syncthreads();
+    lds_barrier();
 
     const int v0 = cfar_run<G, W>(g) * E;   // this thread's run of Doppler rows
     const bool col_on = rv && in_segs(r, a.cv.nseg, a.cv.seg_lo, a.cv.seg_hi);
@@ -1442,12 +1446,12 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     } else {
         float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
         doppler_sums(mag, sums, P, a.cv.ref, v0, v0 + E);
-        __syncthreads();
+        lds_barrier();
         doppler_flags<E>(mag, sums, a.cv, col_on, v0, v0 + E, o);
     }
     RSP_STAMP(1, 4, false);
     if (o.fused && o.rflag) {
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) {
             if (SA != 0) st_u32_sc1(T.hit_count, *s_hits);
             else *T.hit_count = *s_hits;
@@ -1467,7 +1471,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
 // the DMX pair -- both beams' slow-time FFTs, RDM = |X_0| + |X_1|, diff = |X_1| - |X_0|.
 // One MTD workgroup: tile bx (of gx along range) of launch CPI by (of gy); smem / s_hits: the
 // workgroup's dynamic LDS and hit counter.
-template <int P, int REF, int BEAMS>
+template <int P, int REF, int BEAMS, bool JOB>
 __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* __restrict__ rdm,
                                           uint8_t* __restrict__ flagV, const MtdArgs& a, int bx, int by, int gx, int gy,
                                           unsigned char* smem, uint32_t* s_hits) {
@@ -1502,13 +1506,14 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     // one instance of the tile (the kernel's code stays ~half the size: it shares the
     // instruction cache with the PC kernel of the other pipeline); the range job is runtime-
     // guarded -- with n == 0 its hook and finish() return at once
-    const bool job = a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions &&
+    const bool job = JOB && a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions &&
                      (uint64_t)a.prev_nregions * (uint64_t)a.prev_region < (uint64_t)(kOob / 4u);
     RangeJob57 rj;
     RSP_STAMP(1, 0, false);
     RSP_STAMP_RT(1, 8);
     if (job) rj.fetch_idx(a, (int)wg);
-    mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a, job});
+    if constexpr (JOB) mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a});
+    else mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, NoHook{});
     RSP_STAMP(1, 5, false);
     rj.finish(a);
     RSP_STAMP(1, 6, false);
@@ -1518,14 +1523,16 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     RSP_STAMP_RT(1, 9);
 }
 
-template <int P, int REF, int BEAMS>
+// JOB: this launch carries the previous chunk's range stage for the reference's window (the
+// RangeJob57 gathers ride on the tile load); otherwise prev_chunk_hits (if any) runs after the tile.
+template <int P, int REF, int BEAMS, bool JOB>
 __global__ __launch_bounds__((MtdCfg<P, BEAMS>::T), (MtdCfg<P, BEAMS>::WPE)) void mtd_kernel(const float2* __restrict__ pc,
                                                      float* __restrict__ rdm,
                                                      uint8_t* __restrict__ flagV, MtdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_hits;
-    mtd_block<P, REF, BEAMS>(pc, rdm, flagV, a, (int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y, smem,
-                             &s_hits);
+    mtd_block<P, REF, BEAMS, JOB>(pc, rdm, flagV, a, (int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y,
+                                  smem, &s_hits);
 }
 
 // Slow-time DFT for a pulse count without a radix plan (the v2 native P = 332 = 4*83,
@@ -1651,12 +1658,24 @@ static hipError_t launch_mtd_pr(const float2* pc, float* rdm, uint8_t* flagV, in
                                 const MtdArgs& a, hipStream_t s) {
     using C = MtdCfg<P, BEAMS>;
     constexpr size_t lds = C::template lds_for<REF>();
-    static LaunchOnce once;
-    hipError_t e = lds_attr(once, (const void*)mtd_kernel<P, REF, BEAMS>, lds);
-    if (e != hipSuccess) return e;
+    static LaunchOnce once, once_job;
     dim3 grid((unsigned)((a.R_out + C::W - 1) / C::W), (unsigned)ncpi),
         block(C::T);
-    hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS>), grid, block, lds, s, pc, rdm, flagV, a);
+    // the in-launch range job (RangeJob57) only for the reference's range window; any other
+    // previous-chunk range stage runs as prev_chunk_hits in the no-job instance
+    const bool job = REF > 0 && a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 &&
+                     (uint64_t)a.prev_nregions * (uint64_t)a.prev_region < (uint64_t)(kOob / 4u);
+    if constexpr (REF > 0) {
+        if (job) {
+            hipError_t e = lds_attr(once_job, (const void*)mtd_kernel<P, REF, BEAMS, true>, lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS, true>), grid, block, lds, s, pc, rdm, flagV, a);
+            return hipGetLastError();
+        }
+    }
+    hipError_t e = lds_attr(once, (const void*)mtd_kernel<P, REF, BEAMS, false>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((mtd_kernel<P, REF, BEAMS, false>), grid, block, lds, s, pc, rdm, flagV, a);
     return hipGetLastError();
 }
 
