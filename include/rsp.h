@@ -252,10 +252,10 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
                void* stream);
 
 /* ---- execution strategy ------------------------------------------------------------------ */
-/* Overlap-save split of long matched filters (default on): a segment whose FFT exceeds 8192
- * points, with no output that wraps, runs as 4096..8192-point overlap-save blocks instead of
+/* Overlap-save split of long matched filters (default on): a segment whose FFT exceeds 4096
+ * points, with no output that wraps, runs as 2048..8192-point overlap-save blocks instead of
  * one whole-length transform (the same correlation sums; results differ by fp32 rounding).
- * enable = 0 selects the whole-length transforms.  The threshold is fixed (8192 points).
+ * enable = 0 selects the whole-length transforms.  The threshold is fixed (4096 points).
  * RSP_ERR_UNSUPPORTED on a context without the specialised PC kernels (nothing to select). */
 int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable);
 

@@ -39,7 +39,13 @@ struct rsp_ctx {
     hipStream_t stream = nullptr;
     rsp::PcArgs pc{};
     bool pc_v2 = false;                 // per-segment specialised kernels (pc_mf_kernel)
-    int pc_ols_min = 8192;              // overlap-save split of segments longer than this
+#ifndef RSP_PC_OLS_MIN
+// 4096: an 8192-point segment (c4) runs as 3 blocks of 4096 points at four workgroups per CU
+// instead of one whole-row transform at two: PC 289-301 -> 275-282 us per c4 step, chain +1.2-2.3 %
+// (profiles/r04/ab/session9_ols4k.txt; dev-only -D for A/B of the threshold)
+#define RSP_PC_OLS_MIN 4096
+#endif
+    int pc_ols_min = RSP_PC_OLS_MIN;    // overlap-save split of segments longer than this
     std::vector<rsp::PcMfArgs> pc_mf_whole, pc_mf_split;   // per MF segment, for rsp_set_pc_split
     std::vector<rsp::PcMfArgs> pc_mf;   // one launch per matched-filter segment
     rsp::MtdArgs mtd{};

@@ -61,7 +61,7 @@ class Engine:
         capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)
 
     def set_pc_split(self, enable):
-        """Overlap-save blocks for matched filters longer than 8192 points (1, the default) or
+        """Overlap-save blocks for matched filters longer than 4096 points (1, the default) or
         whole-length transforms (0) -- rsp_set_pc_split."""
         capi.check(self.lib.rsp_set_pc_split(self.ctx, int(enable)), self.ctx)
 
