@@ -6,8 +6,8 @@ set -u
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$ROOT"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 for i in 1 2 3; do
-  for v in head ols4k; do
-    RSP_LIB="$ROOT/radar-signal-process_amd/lib/ablate/librsp_$v.so" timeout -k 10 200 python bench.py --config c4 --steps 20 --cpu-seconds 0 > gpurun_out/ab_c4_$v.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/ab_c4_$v.log; exit 1; }
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], d['value'], {k: v['avg_us'] for k, v in r.get('kernels', {}).items()})" gpurun_out/ab_c4_$v.log "c4 $v"
+  for v in ${VARIANTS:-head ols4k}; do
+    RSP_LIB="$ROOT/radar-signal-process_amd/lib/ablate/librsp_$v.so" timeout -k 10 200 python bench.py --config ${CFG:-c4} --steps 20 --cpu-seconds 0 > gpurun_out/ab_${CFG:-c4}_$v.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/ab_${CFG:-c4}_$v.log; exit 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], d['value'], {k: v['avg_us'] for k, v in r.get('kernels', {}).items()})" gpurun_out/ab_${CFG:-c4}_$v.log "${CFG:-c4} $v"
   done
 done
