@@ -193,6 +193,22 @@ def test_mixed_frame_and_cuts(ing):
         _check(ing, stream[:offs[p + 1] - 10], dbf, cfg)
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_long_mixed_frame_walk(ing, seed):
+    """A long frame of randomly mixed record kinds (three record sizes, runs of equal sizes and
+    alternations): the wave's head walk resolves many records per round of candidate loads and
+    must land on every record exactly as the serial walk does."""
+    rng = np.random.default_rng(seed)
+    types = [int(t) for t in rng.choice([0, 1, 2, 3], size=150, p=[0.3, 0.4, 0.2, 0.1])]
+    types[:3] = [1, 1, 1]   # a speculative prefix, then the walk
+    types[40:70] = [0] * 30  # a long run of one size inside the walk
+    dbf, cfg, stream = synth_mixed_frame(types, 100, 9, 9, seed=40 + seed)
+    got, done = _check(ing, stream, dbf, cfg)
+    assert done
+    want, _, _, _ = ref.FrameReader().read(ref.BytesStream(stream), dbf, cfg, 0)
+    _exact_rows(got, want, types)
+
+
 def test_dbf24_size_error_and_ddc_only(ing):
     """14 channels give an odd 24-bit value count: a MATLAB size error in the reference,
     RSP_PRT_BAD_SHAPE here; rsp_ingest_ddc_dev refuses the first non-DDC record."""
