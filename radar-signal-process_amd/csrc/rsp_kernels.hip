@@ -1270,6 +1270,14 @@ __device__ __forceinline__ void own_rows(int g, int lo, int hi, const F& fn) {
     for (int mm = a0; mm < b0; ++mm) fn(mm);
 }
 
+// MTD load-phase wave priority (round 4, profiles/r04/ab/session11_mtd_prio.txt): for Doppler
+// lengths P >= 256 a tile's waves run at priority 3 until the tile's loads are issued (mtd_block
+// raises it, mtd_tile drops it before the FFT), so a newly resident workgroup gets its loads out
+// ahead of the other tiles' compute: c4 MTD 690-707 -> 658-663 us, c4 +3.5 %, outputs identical.
+// At P = 128 (c3) the same cost 1-2 %, and in the PC kernel 10 % (its rows' compute is the long
+// phase), so neither has it.
+constexpr int kMtdLoadPrio = 3, kMtdLoadPrioMinP = 256;
+
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
 // after_loads(): called once the tile's first-beam loads are issued (RangeJob57 gathers).
@@ -1347,6 +1355,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         }
         if (b == 0 && !(kMtdDma<P, BEAMS, LA, W>() && a.mti_lag <= 0)) after_loads();
         RSP_STAMP(1, 1, true);
+        if constexpr (P >= kMtdLoadPrioMinP) __builtin_amdgcn_s_setprio(0);   // the tile's loads are out
         fft_reg_w<P, G, 1, E, 0, NW>(u, reinterpret_cast<float2*>(smem) + c * C::SLOT, g, tw);
         RSP_STAMP(1, 2, false);
         if constexpr (BEAMS == 2) {
@@ -1510,6 +1519,7 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
                      (uint64_t)a.prev_nregions * (uint64_t)a.prev_region < (uint64_t)(kOob / 4u);
     RangeJob57 rj;
     RSP_STAMP(1, 0, false);
+    if constexpr (P >= kMtdLoadPrioMinP) __builtin_amdgcn_s_setprio(kMtdLoadPrio);
     RSP_STAMP_RT(1, 8);
     if (job) rj.fetch_idx(a, (int)wg);
     if constexpr (JOB) mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a});
