@@ -1276,7 +1276,13 @@ __device__ __forceinline__ void own_rows(int g, int lo, int hi, const F& fn) {
 // ahead of the other tiles' compute: c4 MTD 690-707 -> 658-663 us, c4 +3.5 %, outputs identical.
 // At P = 128 (c3) the same cost 1-2 %, and in the PC kernel 10 % (its rows' compute is the long
 // phase), so neither has it.
-constexpr int kMtdLoadPrio = 3, kMtdLoadPrioMinP = 256;
+#ifndef RSP_MTD_PRIO
+#define RSP_MTD_PRIO 3      // (dev-only -D for A/B)
+#endif
+#ifndef RSP_MTD_PRIO_MINP
+#define RSP_MTD_PRIO_MINP 256
+#endif
+constexpr int kMtdLoadPrio = RSP_MTD_PRIO, kMtdLoadPrioMinP = RSP_MTD_PRIO_MINP;
 
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
