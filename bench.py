@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--prefilter", action="store_true",
                     help="fused iSTC (a synthetic stc curve) + MTI lag 30 in the chain (rsp_set_prefilter)")
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
+    ap.add_argument("--flow", type=int, default=None,
+                    help="rsp_set_flow schedule: 0 chunked pipelines, 1/2 one persistent dataflow launch "
+                         "(default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--profile-every", type=int, default=7,
@@ -783,6 +786,8 @@ def main():
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
+    if args.flow is not None:
+        eng.set_flow(args.flow)
     if args.prefilter:
         import numpy as np
         from rsp.prefilter import istc_gain

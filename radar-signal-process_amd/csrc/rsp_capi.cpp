@@ -16,6 +16,8 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <exception>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -67,6 +69,10 @@ struct rsp_ctx {
     DevBuf pf_gain;                     // fused iSTC gains (rsp_set_prefilter)
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
+    // persistent dataflow (rsp_set_flow): scratch ring, hit-list ring, counts, control words,
+    // RDM ring (when the caller takes no RDM)
+    int flow = 0;
+    DevBuf fl_ring, fl_hring, fl_hcount, fl_ctl, fl_rdm;
     DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
     DevBuf ing_meta;                    // ingest: per-PRT record offsets and types
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging (rsp_cfar)
@@ -292,7 +298,8 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
-                      &ctx->meas_band, &ctx->ing_meta};
+                      &ctx->meas_band, &ctx->ing_meta, &ctx->fl_ring, &ctx->fl_hring, &ctx->fl_hcount,
+                      &ctx->fl_ctl, &ctx->fl_rdm};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -714,6 +721,28 @@ int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis) {
 }
 
 
+static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess; }
+
+int rsp_set_flow(rsp_ctx* ctx, int32_t mode) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_flow: null ctx");
+    if (mode < 0 || mode > 2) return fail(ctx, RSP_ERR_ARG, "rsp_set_flow: mode must be 0..2");
+    ctx->flow = mode;
+    return RSP_OK;
+}
+
+int rsp_flow_status(rsp_ctx* ctx, int32_t* timed_out) {
+    if (!ctx || !timed_out) return fail(ctx, RSP_ERR_ARG, "rsp_flow_status: null argument");
+    *timed_out = 0;
+    if (!ctx->fl_ctl.p) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    uint32_t w = 0;
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    HIP_TRY(ctx, hipMemcpy(&w, (const char*)ctx->fl_ctl.p + (size_t)(rsp::kFlowCtlLines - 1) * rsp::kFlowLine * 4, 4,
+                           hipMemcpyDeviceToHost));
+    *timed_out = (int32_t)w;
+    return RSP_OK;
+}
+
 static int64_t chunk_of(const rsp_ctx* ctx, int64_t batch) {
     int64_t c = ctx->chunk;
     if (c <= 0) {
@@ -800,7 +829,6 @@ static int build_cfar(rsp_ctx* ctx, const rsp_cfar_params* cf, int64_t V, int64_
     return RSP_OK;
 }
 
-static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess; }
 
 // Order this call's use of the context scratch after the previous call's (on any stream).
 static int scratch_acquire(rsp_ctx* ctx, hipStream_t s) {
@@ -931,6 +959,63 @@ int rsp_set_prefilter(rsp_ctx* ctx, const float* gain, int32_t mti_lag) {
     return RSP_OK;
 }
 
+// The whole call as one persistent dataflow launch (rsp_set_flow; FlowArgs in rsp_internal.h).
+// RSP_ERR_UNSUPPORTED (without touching the error text) when the context or call is outside what
+// the dataflow kernel is built for -- the caller then runs the chunked pipeline.
+static int run_flow(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncpi, const rsp::MtdArgs& m,
+                    const rsp::CfarRArgs& cr, bool cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
+                    hipStream_t s) {
+    const int64_t P = ctx->p.P, Ro = ctx->p.R_out;
+    if (!ctx->pc_v2 || ctx->pc_mf.size() != 2 || ctx->beams != 1 || ctx->V != P || m.pin != P || m.bnf > 0 ||
+        m.mti_lag > 0 || ctx->pc_mf[0].gain || ctx->pc_mf[1].gain ||
+        !rsp::flow_supported((int)P, ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft, dtype, ctx->beams))
+        return RSP_ERR_UNSUPPORTED;
+    if (cfar && !(m.cv.ref == 5 && m.cv.save == 7 && (!cr.rflag || (cr.ref == 5 && cr.save == 7))))
+        return RSP_ERR_UNSUPPORTED;
+    if (ncpi > 0x7fffffff / 2) return RSP_ERR_UNSUPPORTED;
+    int nreg = 0, reg = 0;
+    rsp::mtd_regions((int)P, (int)Ro, 1, &nreg, &reg, 1);   // per CPI: tiles, entries per tile
+    constexpr int64_t Q = rsp::kFlowQueues, S = rsp::kFlowSlots;
+    const int64_t Qn = ncpi < Q ? ncpi : Q;                 // queues in use
+    const size_t plane = (size_t)P * Ro;
+    int rc;
+    if ((rc = ensure(ctx, ctx->fl_ring, (size_t)Qn * S * plane * sizeof(float2)))) return rc;
+    if ((rc = ensure(ctx, ctx->fl_ctl, (size_t)rsp::kFlowCtlLines * rsp::kFlowLine * sizeof(uint32_t)))) return rc;
+    const bool hits = cfar && cr.rflag;
+    if (hits) {
+        if ((rc = ensure(ctx, ctx->fl_hring, (size_t)Qn * S * nreg * reg * sizeof(uint32_t)))) return rc;
+        if ((rc = ensure(ctx, ctx->fl_hcount, (size_t)Qn * S * nreg * sizeof(uint32_t)))) return rc;
+    }
+    if (!d_rdm && (rc = ensure(ctx, ctx->fl_rdm, (size_t)Qn * S * plane * sizeof(float)))) return rc;
+    rsp::FlowArgs f;
+    std::memset(&f, 0, sizeof(f));
+    f.echo = d_echo;
+    f.a1 = ctx->pc_mf[0];
+    f.a2 = ctx->pc_mf[1];
+    f.a1.rows = f.a2.rows = (int)P;
+    f.m = m;
+    f.m.flag_zero = 1;
+    f.m.rflag = cr.rflag;
+    f.m.flag = nullptr;
+    f.m.hits = nullptr;
+    f.m.hit_count = nullptr;
+    f.m.prev_nregions = 0;
+    f.cr = cr;
+    f.ring = (float2*)ctx->fl_ring.p;
+    f.hring = hits ? (uint32_t*)ctx->fl_hring.p : nullptr;
+    f.hcount = hits ? (uint32_t*)ctx->fl_hcount.p : nullptr;
+    f.rdm_ring = d_rdm ? 0 : 1;
+    f.rdm = d_rdm ? d_rdm : (float*)ctx->fl_rdm.p;
+    f.flag = cfar ? d_flag : nullptr;
+    f.flagV = cfar ? d_flagV : nullptr;
+    f.ctl = (uint32_t*)ctx->fl_ctl.p;
+    f.ncpi = (int)ncpi;
+    f.order = ctx->flow;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->fl_ctl.p, 0, ctx->fl_ctl.n, s));
+    HIP_TRY(ctx, timed(ctx, RSP_K_FLOW, s, [&] { return rsp::launch_flow(f, dtype, s); }));
+    return RSP_OK;
+}
+
 // The chain over `units` on stream s.  win == 0: a unit is one CPI ([P][R] input rows).
 // win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
 // frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
@@ -947,6 +1032,10 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         if (rc) return rc;
     } else {
         m.cv.enabled = 0;
+    }
+    if (ctx->flow > 0 && win == 0 && !pc_input && !d_diff) {
+        const int rc = run_flow(ctx, d_echo, dtype, units, m, cr, cfar != nullptr, d_rdm, d_flag, d_flagV, s);
+        if (rc != RSP_ERR_UNSUPPORTED) return rc;   // (not this shape: the chunked pipeline below)
     }
     const int64_t ocpi = win > 0 ? win : 1;               // output CPIs per unit
     m.nwin = win;
@@ -1410,6 +1499,9 @@ static int host_pipe_init(rsp_ctx* ctx) {
     return RSP_OK;
 }
 
+// (thread creation can throw: callers run inside rsp_pc_mtd_cfar's try block, which turns any
+// exception into an error status -- nothing may unwind through the extern "C" boundary into
+// the MEX host)
 static rsp::CopyPool& host_pool(rsp_ctx* ctx) {
     auto& h = ctx->hp;
     int want = h.threads;
@@ -1417,7 +1509,10 @@ static rsp::CopyPool& host_pool(rsp_ctx* ctx) {
         const unsigned hc = std::thread::hardware_concurrency();
         want = hc >= 16 ? 8 : (hc >= 4 ? (int)hc / 2 : 1);
     }
-    if (!h.pool || h.pool->threads() != want) h.pool.reset(new rsp::CopyPool(want));
+    if (!h.pool || h.pool->threads() != want) {
+        h.pool.reset();
+        h.pool.reset(new rsp::CopyPool(want));
+    }
     return *h.pool;
 }
 
@@ -1503,10 +1598,38 @@ int rsp_set_host_pipeline(rsp_ctx* ctx, int64_t cpis_per_chunk, int32_t copy_thr
     return RSP_OK;
 }
 
+static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                      int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
+                      uint8_t* flag_out, uint8_t* flagV_out);
+
 int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
                     int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
                     uint8_t* flag_out, uint8_t* flagV_out) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "null ctx");
+    int rc;
+    try {
+        rc = host_chain(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out);
+    } catch (const std::bad_alloc&) {
+        rc = fail(ctx, RSP_ERR_NOMEM, "rsp_pc_mtd_cfar: host allocation failed");
+    } catch (const std::exception& e) {
+        rc = fail(ctx, RSP_ERR_NOMEM, "rsp_pc_mtd_cfar: host pipeline: %s", e.what());
+    } catch (...) {
+        rc = fail(ctx, RSP_ERR_NOMEM, "rsp_pc_mtd_cfar: host pipeline: unknown exception");
+    }
+    if (rc && ctx->hp.s_h2d) {
+        // an error after chunks were issued: drain all three streams before returning, so the
+        // next call's first H2D cannot overwrite an input slot a chain still reads, nor its
+        // output staging race a D2H still in flight (the status stays the first error's)
+        (void)hipStreamSynchronize(ctx->hp.s_h2d);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->hp.s_d2h);
+    }
+    return rc;
+}
+
+static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                      int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
+                      uint8_t* flag_out, uint8_t* flagV_out) {
     int rc = check_host_call(ctx, echo, dtype, layout, P, R, batch);
     if (rc) return rc;
     if (out_layout != RSP_ROWMAJOR && out_layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad out_layout");

@@ -15,17 +15,18 @@ namespace rsp {
 
 class CopyPool {
 public:
+    // Thread creation can throw (std::system_error / bad_alloc): the threads already started are
+    // stopped and joined before the exception leaves, so no joinable std::thread is destroyed.
     explicit CopyPool(int threads) : n_(threads < 1 ? 1 : threads) {
-        for (int i = 1; i < n_; ++i) workers_.emplace_back([this, i] { loop(i); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
+        try {
+            workers_.reserve((size_t)n_);
+            for (int i = 1; i < n_; ++i) workers_.emplace_back([this, i] { loop(i); });
+        } catch (...) {
+            stop_all();
+            throw;
         }
-        cv_.notify_all();
-        for (auto& w : workers_) w.join();
     }
+    ~CopyPool() { stop_all(); }
     int threads() const { return n_; }
 
     // memcpy(dst, src, bytes) split into n_ page-aligned parts; the caller runs part 0 and
@@ -69,6 +70,16 @@ public:
 
 private:
     static constexpr int kMinSplit = 1 << 20;
+    void stop_all() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_)
+            if (w.joinable()) w.join();
+        workers_.clear();
+    }
     void part(int i) {
         const size_t a = (size_t)i * per_;
         if (a >= n_items_) return;

@@ -147,6 +147,39 @@ struct MtdArgs {
     CfarRArgs prev_cr;
 };
 
+// Persistent PC -> MTD (+ Doppler CFAR) -> range CFAR dataflow (rsp_set_flow, flow_kernel in
+// rsp_kernels.hip): one launch per call.  CPI c belongs to queue c % kFlowQueues (one per XCD);
+// a queue's items are PC units of its CPIs, MTD tiles (each carrying the range job of the
+// queue's previous CPI) and, after its last CPI, range-only items.  The PC rows of a CPI go to a
+// ring of kFlowSlots scratch slots per queue; hand-offs between workgroups are write-through
+// (sc1 stores, drained, one counter add per item) and read with sc1 loads.
+constexpr int kFlowQueues = 8;
+constexpr int kFlowSlots = 3;
+constexpr int kFlowLine = 32;   // uint32 per control line (128 B)
+// control words: heads [kFlowQueues], counters [kFlowQueues][kFlowSlots][2] (PC units, MTD
+// tiles done), then the status line (a wait that timed out)
+constexpr int kFlowCtlLines = kFlowQueues + kFlowQueues * kFlowSlots * 2 + 1;
+struct FlowArgs {
+    const void* echo;      // [ncpi][P][R] (complex fp32 or fp16 I/Q)
+    PcMfArgs a1, a2;       // the short (FIR + MF) and the long matched-filter segment, rows = P
+    MtdArgs m;             // tile arguments (its per-launch pointers are unused)
+    CfarRArgs cr;          // range stage (cr.rflag && m.cv.enabled: range jobs run)
+    float2* ring;          // [kFlowQueues][kFlowSlots][P][R_out] PC rows
+    uint32_t* hring;       // [kFlowQueues][kFlowSlots][nm][region] Doppler hit lists
+    uint32_t* hcount;      // [kFlowQueues][kFlowSlots][nm]
+    float* rdm;            // [ncpi][V][R_out] output, or the RDM ring [kFlowQueues][kFlowSlots][V][R_out]
+    int rdm_ring;
+    uint8_t* flag;         // [ncpi][V][R_out] or null (no CFAR)
+    uint8_t* flagV;        // [ncpi][V][R_out] or null
+    uint32_t* ctl;         // kFlowCtlLines lines, zeroed before the launch
+    int ncpi;
+    int nl, nsh, nm;       // per CPI: long-row units, short-row groups, MTD tiles
+    int region;            // hit-list entries per tile
+    int order;             // 1: a CPI's MTD tiles after the next CPI's PC units; 2: the two interleaved
+};
+bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams);
+hipError_t launch_flow(FlowArgs& a, int dtype, hipStream_t s);
+
 // Raw-data ingest (rsp_ingest.hip): one frame of uniform DDC PRT records.
 // motionParaMeasure.m's scalar arguments (rsp_measure_params, rsp_measure.hip).
 struct MeasureArgs {

@@ -448,141 +448,6 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     RSP_STAMP_RT(0, 9);
 }
 
-#if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
-// Persistent long rows with an LDS-DMA prefetch ring (dev-only -DRSP_PC_DMA=2, A/B of VERDICT r3
-// item 1, variant "persistent grid, 2-slot LDS ring"): each workgroup owns two padded row slots
-// (2 workgroups per CU) and walks rows first, first + step, ...  Row k computes in slot k % 2
-// while row k+1's input lands in the other slot by buffer_load_dwordx4 ... lds, issued right
-// after the barrier that opens row k.  The DMA and the spectrum loads are inline asm, invisible
-// to hipcc's waitcnt pass (a compiler-visible LDS-DMA makes every later barrier or LDS fence
-// wait vmcnt(0), draining the prefetch), so every wait on them is counted here by hand: the
-// only compiler-visible VMEM operations inside the loop are the row's stores.
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ v4i_t rsrc_words(const void* base, uint32_t bytes) {
-    const uint64_t p = (uint64_t)base;
-    v4i_t r;
-    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
-    r.y = __builtin_amdgcn_readfirstlane((int)((p >> 32) & 0xffffu));
-    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
-    r.w = 0x00020000;
-    return r;
-}
-__device__ __forceinline__ void dma16_asm(v4i_t rs, uint32_t voff, uint32_t lds_byte) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(rs), "s"(lds_byte)
-                 : "memory");
-}
-__device__ __forceinline__ float2 ld8_asm(v4i_t rs, uint32_t voff, uint32_t soff) {
-    float2 v;
-    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rs), "s"(soff) : "memory");
-    return v;
-}
-// s_waitcnt vmcnt(K) that also (re)defines the registers an asm load wrote, so no use of them is
-// scheduled above the wait
-template <int K>
-__device__ __forceinline__ void vm_wait16(float2 (&h)[16]) {
-    asm volatile("s_waitcnt vmcnt(%16)"
-                 : "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]), "+v"(h[7]),
-                   "+v"(h[8]), "+v"(h[9]), "+v"(h[10]), "+v"(h[11]), "+v"(h[12]), "+v"(h[13]), "+v"(h[14]), "+v"(h[15])
-                 : "n"(K)
-                 : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_byte(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-template <int N, int G>
-__device__ __forceinline__ void pc_long_persist(const float2* __restrict__ echo, float2* __restrict__ out,
-                                                const PcMfArgs& a, int first, int step, float2* lds) {
-    constexpr int E = N / G;
-    static_assert(E == 16 && G % 64 == 0, "persistent PC rows: 16 elements per thread, whole waves");
-    constexpr int SLOT = padded_len(N);
-    constexpr int NQ = N * 8 / (G * 16);   // DMA pieces per thread per row
-    const int t = threadIdx.x;
-    const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
-    const int ns = a.nsub > 1 ? a.nsub : 1;
-    const int nun = a.rows * ns;
-    constexpr int NW = tw_regs<N, E>() > 0 ? tw_regs<N, E>() : 1;
-    float2 w[NW];
-    tw_preload<N, G, 1, E, 0, NW>(w, t, a.mf.tw);
-#pragma unroll
-    for (int i = 0; i < NW; ++i) asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[i]) : : "memory");
-    const v4i_t rh = rsrc_words(a.mf.H, (uint32_t)N * 8u);
-    struct Geo {
-        const float2* x;
-        float2* y;
-        uint32_t in_bytes, out_bytes;
-    };
-    auto geo = [&](int u) {
-        const int row = __builtin_amdgcn_readfirstlane(u / ns), sub = __builtin_amdgcn_readfirstlane(u % ns);
-        int in_start = a.mf.in_start, in_len = a.mf.in_len, out_start = a.mf.out_start, out_len = a.mf.out_len;
-        if (a.nsub > 1) {
-            const int off = sub * a.sub_step;
-            in_start += off;
-            out_start += off;
-            in_len = max(0, min(in_len - off, N));
-            out_len = max(0, min(out_len - off, a.sub_step));
-        }
-        Geo g;
-        g.x = echo + (size_t)row * a.R + __builtin_amdgcn_readfirstlane(in_start);
-        g.y = out + (size_t)row * a.R_out + __builtin_amdgcn_readfirstlane(out_start);
-        g.in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(in_len) * 8u;
-        g.out_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(out_len) * 8u;
-        return g;
-    };
-    // a row's input: NQ 16-byte pieces into `slot` (the range check is per dword, so a piece
-    // straddling in_len keeps its in-range element)
-    auto issue = [&](const Geo& g, float2* slot) {
-        const v4i_t rx = rsrc_words(g.x, g.in_bytes);
-        const uint32_t base = lds_byte(slot);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) dma16_asm(rx, (uint32_t)(q * G + t) * 16u, base + (uint32_t)(q * G + wb) * 16u);
-    };
-    // (slot k is lds + k * SLOT -- an offset from the LDS array, so the accesses stay ds_*: a
-    // pointer picked from an array of two made hipcc fall back to flat loads and stores)
-    int k = 0;
-    Geo g = geo(first < nun ? first : 0);
-    if (first < nun) issue(g, lds);
-    bool head = true;
-    for (int u = first; u < nun; u += step, k ^= 1) {
-        float2 hs[E];
-#pragma unroll
-        for (int m = 0; m < E; ++m) hs[m] = ld8_asm(rh, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-        // this row's pieces are older than: (not the first row) the previous row's E stores, and
-        // the E spectrum loads just issued
-        if (head) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * E) : "memory");
-        head = false;
-        float2* cur = lds + k * SLOT;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        // every wave is past the previous row (its last reads of the other slot) and this row
-        // has landed: prefetch the next row into the other slot
-        const Geo gr = g;
-        const bool more = u + step < nun;
-        if (more) {
-            g = geo(u + step);
-            issue(g, lds + (k ^ 1) * SLOT);
-        }
-        float2 v[E];
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = cur[t + G * m];
-        fft_reg_w<N, G, 1, E, 0, NW, false>(v, cur, t, w);
-        // the spectrum loads are older than the next row's NQ pieces
-        if (more) vm_wait16<NQ>(hs);
-        else vm_wait16<0>(hs);
-#pragma unroll
-        for (int m = 0; m < E; m += 2) cmul2_conj(v[m], v[m], hs[m], v[m + 1], v[m + 1], hs[m + 1]);
-        fft_reg_w<N, G, 1, E, 0, NW, false>(v, cur, t, w);
-        const auto yr = buf_rsrc(gr.y, gr.out_bytes);
-#pragma unroll
-        for (int m = 0; m < E; ++m) buf_st_f2(cconj(v[m]), yr, (uint32_t)t * 8u, (uint32_t)(G * m) * 8u);
-    }
-}
-#endif
 
 // Workgroup size shared by a pair of segment lengths: both run T threads (RPB = T/G rows).
 template <int N1, int N2>
@@ -605,17 +470,6 @@ __device__ __forceinline__ void pc_mf_block(const TIn* __restrict__ echo, float2
     using PC = PairCfg<N1, M2>;
     // unit u of a segment = (row u / nsub, overlap-save sub-block u % nsub)
     if constexpr (N2 != 0) {
-#if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
-        if constexpr (std::is_same<TIn, float2>::value && PcCfg<N2>::G == PC::T && N2 <= 4096) {
-            if (nblk2 < 0) {   // the host chose the persistent form: -nblk2 workgroups walk the long rows
-                if (bid < -nblk2) {
-                    pc_long_persist<N2, PcCfg<N2>::G>(echo, out, a2, bid, -nblk2, lds);
-                    return;
-                }
-                nblk2 = -nblk2;
-            }
-        }
-#endif
         if (bid < nblk2) {
             constexpr int G = PcCfg<N2>::G;
             const int grp = threadIdx.x / G, t = threadIdx.x % G;
@@ -676,27 +530,6 @@ static hipError_t launch_pc_mf_n(const TIn* echo, float2* out, const PcMfArgs& a
     const int u2 = a2 ? a2->rows * (a2->nsub > 1 ? a2->nsub : 1) : 0;
     const int nblk2 = N2 ? (u2 + PC::RPB2 - 1) / PC::RPB2 : 0;
     dim3 grid((unsigned)(nblk1 + nblk2)), block(PC::T);
-#if defined(RSP_PC_DMA) && RSP_PC_DMA >= 2
-    if constexpr (std::is_same<TIn, float2>::value && N2 != 0 && N2 <= 4096 && PcCfg<M2>::G == PC::T) {
-        if (a2 && a2->gain == nullptr && nblk2 > 0) {   // persistent long rows: 2 workgroups per CU
-            static int cus = 0;
-            if (!cus) {
-                int dev = 0;
-                if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
-                if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorInvalidDevice;
-            }
-            const int nper = u2 < 2 * cus ? u2 : 2 * cus;
-            constexpr size_t L2X = 2 * (size_t)PcCfg<M2>::SLOT * sizeof(float2);
-            constexpr size_t LX = L2X > PC::lds ? L2X : PC::lds;
-            static LaunchOnce once_p;
-            e = lds_attr(once_p, (const void*)pc_mf_kernel<TIn, N1, N2>, LX);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), dim3((unsigned)(nblk1 + nper)), block, LX, s, echo, out, a1,
-                               *a2, -nper);
-            return hipGetLastError();
-        }
-    }
-#endif
     hipLaunchKernelGGL((pc_mf_kernel<TIn, N1, N2>), grid, block, lds, s, echo, out, a1, a2 ? *a2 : a1, nblk2);
     return hipGetLastError();
 }
@@ -1110,7 +943,24 @@ __device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nw
 // r+7 .. r+13) right after the tile's own loads,
 // and the test + first-maximum scatter run after the tile -- the three dependent gathers hide
 // under the tile's FFT and Doppler CFAR instead of trailing the workgroup.
-struct RangeJob57 {
+// Where a range job reads and writes: the previous chunk's RDM / flag planes, hit lists and
+// counts (MtdArgs::prev_* in the chunked pipeline; the dataflow kernel's ring slots otherwise).
+struct RangeSrc {
+    const float* rdm;
+    uint8_t* flag;
+    const uint32_t* hits;
+    const uint32_t* count;
+    int region;
+    const CfarRArgs& cr;
+    __device__ __forceinline__ static RangeSrc of(const MtdArgs& a) {
+        return RangeSrc{a.prev_rdm, a.prev_flag, a.prev_hits, a.prev_count, a.prev_region, a.prev_cr};
+    }
+};
+
+// LA: cache policy of the job's loads (kSc1 when the hit lists and the RDM were written by other
+// workgroups of the same launch).
+template <int LA = 0>
+struct RangeJob57T {
     // the cells executeCFAR's fixCells test of r-1, r, r+1 reads (5 reference cells beyond 7 guard
     // cells on each side): r-13 .. r-7, r-1 .. r+1, r+7 .. r+13
     static constexpr int NX = 17;
@@ -1125,7 +975,7 @@ struct RangeJob57 {
 #pragma unroll
         for (int k = 0; k < NX; ++k) {
             const int q = r + cell_off(k);
-            x[k] = buf_ld_f(rr, (uint32_t)q < rlive ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
+            x[k] = buf_ld_fa<LA>(rr, (uint32_t)q < rlive ? (rowoff + (uint32_t)q) * 4u : kOob, 0u);
         }
     }
     // executeCFAR.m:45-84 at hit column r: the fixCells test of r-1, r, r+1 (one-sided windows
@@ -1153,46 +1003,48 @@ struct RangeJob57 {
     }
     uint32_t n = 0, idx = 0;
     float x[NX];
-    __device__ __forceinline__ void fetch_idx(const MtdArgs& a, int rg) {
+    __device__ __forceinline__ void fetch_idx(const RangeSrc& s, int rg) {
         // both loads issue at once: a region holds W*P >= blockDim entries, so the index load
         // is in bounds (and ignored) past the count -- no count -> index round trip
-        n = a.prev_count[rg];
-        idx = a.prev_hits[(size_t)rg * a.prev_region + threadIdx.x];
+        n = ld_u32<LA>(s.count + rg);
+        idx = ld_u32<LA>(s.hits + (size_t)rg * s.region + threadIdx.x);
     }
-    __device__ __forceinline__ void fetch_cells(const MtdArgs& a) {
+    __device__ __forceinline__ void fetch_cells(const RangeSrc& s) {
         // Every wave of every MTD workgroup issues these 17 loads, unconditionally: a lane
         // without a cell (no hit, no job) loads through the buffer range check (voffset kOob:
         // 0, no memory access).  A branch around them would leave the waits of the tile's FFT
         // (vmcnt counts in issue order) merged from two paths, so a wave with hits would wait
         // for its gathers before its first butterfly (c3: 3.8 us per 16-CPI launch).
-        const CfarRArgs& c = a.prev_cr;
+        const CfarRArgs& c = s.cr;
         const bool mine = threadIdx.x < n;
         const uint32_t R = c.R > 0 ? (uint32_t)c.R : 1u, V = c.V > 0 ? (uint32_t)c.V : 1u;   // (no job: unset)
         const uint32_t row = idx / R;
         const int r = (int)(idx - row * R);
         const int v = (int)(row % V);
         const bool zrow = v >= c.cz_lo && v < c.cz_hi;
-        gather(x, buf_rsrc(a.prev_rdm, kOob), row, r, mine && !zrow, c.R);   // (job => the RDM is < kOob bytes)
+        gather(x, buf_rsrc(s.rdm, kOob), row, r, mine && !zrow, c.R);   // (job => the RDM is < kOob bytes)
     }
-    __device__ __forceinline__ void finish(const MtdArgs& a) {
+    __device__ __forceinline__ void finish(const RangeSrc& s) {
         if (threadIdx.x >= n) return;
-        const CfarRArgs& c = a.prev_cr;
+        const CfarRArgs& c = s.cr;
         const uint32_t row = idx / (uint32_t)c.R;
         const int r = (int)(idx - row * (uint32_t)c.R);
         int slo, shi;
         seg_of(r, c.nseg, c.seg_lo, c.seg_hi, slo, shi);
         if (shi <= slo) return;
         const int best = test(x, r, slo, shi, c);
-        if (best >= 0) a.prev_flag[(size_t)row * c.R + best] = 1;
+        if (best >= 0) s.flag[(size_t)row * c.R + best] = 1;
     }
 };
+using RangeJob57 = RangeJob57T<0>;
 
-struct RangeHook {   // mtd_tile's after_loads(): the range job's gathers (a workgroup without a
-                     // job, rj.n == 0, issues them with every lane out of range)
-    RangeJob57& rj;
-    const MtdArgs& a;
-    static constexpr int kLoads = RangeJob57::kLoads;
-    __device__ __forceinline__ void operator()() const { rj.fetch_cells(a); }
+template <int LA = 0>
+struct RangeHookT {   // mtd_tile's after_loads(): the range job's gathers (a workgroup without a
+                      // job, rj.n == 0, issues them with every lane out of range)
+    RangeJob57T<LA>& rj;
+    const RangeSrc& s;
+    static constexpr int kLoads = RangeJob57T<LA>::kLoads;
+    __device__ __forceinline__ void operator()() const { rj.fetch_cells(s); }
 };
 
 struct NoHook {
@@ -1344,7 +1196,9 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             for (int m = 0; m < E; ++m) asm volatile("" : "+v"(wv[m]));
 #pragma unroll
             for (int i = 0; i < NW; ++i) asm volatile("" : "+v"(tw[i]));
-            __builtin_amdgcn_s_barrier();
+            // (the barrier as asm with a memory clobber: __builtin_amdgcn_s_barrier touches no
+            // memory at the IR level, so nothing would keep the LDS reads below it)
+            asm volatile("s_barrier" ::: "memory");
             const float2* l = reinterpret_cast<const float2*>(smem);
 #pragma unroll
             for (int m = 0; m < E; ++m) {
@@ -1385,7 +1239,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
                 const int c0 = T.bx * W + (i % SEG) * 16;
                 if (c0 < (int)R)
                     __builtin_amdgcn_raw_buffer_store_b128(v4i{0, 0, 0, 0}, fz, (uint32_t)(i / SEG) * R + (uint32_t)c0,
-                                                           0u, 0);
+                                                           0u, SA);
             }
             bg_done = true;
         }
@@ -1524,14 +1378,15 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     const bool job = JOB && a.prev_nregions > 0 && a.prev_cr.ref == 5 && a.prev_cr.save == 7 && (int)wg < a.prev_nregions &&
                      (uint64_t)a.prev_nregions * (uint64_t)a.prev_region < (uint64_t)(kOob / 4u);
     RangeJob57 rj;
+    const RangeSrc rs = RangeSrc::of(a);
     RSP_STAMP(1, 0, false);
     if constexpr (P >= kMtdLoadPrioMinP) __builtin_amdgcn_s_setprio(kMtdLoadPrio);
     RSP_STAMP_RT(1, 8);
-    if (job) rj.fetch_idx(a, (int)wg);
-    if constexpr (JOB) mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHook{rj, a});
+    if (job) rj.fetch_idx(rs, (int)wg);
+    if constexpr (JOB) mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, RangeHookT<0>{rj, rs});
     else mtd_tile<P, REF, BEAMS, 0, 0>(T, a, smem, s_hits, NoHook{});
     RSP_STAMP(1, 5, false);
-    rj.finish(a);
+    rj.finish(rs);
     RSP_STAMP(1, 6, false);
     if (job ? (rj.n > blockDim.x || a.prev_nregions > nwg) : a.prev_nregions > 0)
         prev_chunk_hits(a, (int)wg, nwg, job ? (int)blockDim.x : 0);
@@ -1799,6 +1654,262 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
         case 1536: return launch_mtd_p<1536>(pc, rdm, flagV, ncpi, a, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+// ================================================================== persistent dataflow
+// PC -> MTD (+ Doppler CFAR) -> range CFAR of a whole call in ONE launch (rsp_set_flow; VERDICT r4
+// item 1: the corner turn without launch boundaries).  FlowArgs (rsp_internal.h) describes the
+// queues.  Resident workgroups claim items from the queue of their own XCD (HW_REG_XCC_ID), so a
+// CPI's PC rows and its MTD tiles normally share one L2, and steal from the other queues once
+// theirs is drained (placement changes speed only: every hand-off is placement-independent).
+// Per queue the item order is PC(0), then for each CPI j: PC(j+1) and MTD(j) (in that order, or
+// interleaved), then the range-only items of the last CPI; every dependency points to an earlier
+// item of the same queue, and items are claimed in queue order by running workgroups, so the
+// smallest unfinished item can always run.
+//   PC unit of CPI j      waits until MTD(j - kFlowSlots) is done with the scratch slot
+//   MTD tile of CPI j     waits for PC(j) (all units), MTD(j-1) (its range job reads that CPI's
+//                         RDM and hit list), MTD(j-kFlowSlots+1) (hit-list / RDM slot reuse)
+//   range-only item       waits for MTD(J-1)
+// Hand-offs follow MI355X_MICROARCH.md's write-through form: every handed-off byte (PC rows, RDM,
+// flag background, hit lists and counts) is stored sc1, every storing wave drains vmcnt before
+// its workgroup's one relaxed counter add, and every load of such bytes is an sc1 load issued
+// after thread 0 saw the counter and the workgroup barrier.  Every wait is bounded (0.5 s; the
+// status word then records it and no later wait blocks), so a protocol fault ends the launch.
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v & (uint32_t)(kFlowQueues - 1);
+}
+__device__ __forceinline__ uint32_t* flow_head(uint32_t* ctl, int q) { return ctl + q * kFlowLine; }
+__device__ __forceinline__ uint32_t* flow_ctr(uint32_t* ctl, int q, int slot, int k) {
+    return ctl + (kFlowQueues + (q * kFlowSlots + slot) * 2 + k) * kFlowLine;
+}
+__device__ __forceinline__ uint32_t* flow_status(uint32_t* ctl) { return ctl + (kFlowCtlLines - 1) * kFlowLine; }
+
+// thread 0: wait until *p >= target (relaxed sc1 polls, s_sleep between)
+__device__ __forceinline__ void flow_wait(uint32_t* p, uint32_t target, uint32_t* st) {
+    if (ld_u32<kSc1>(p) >= target) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (ld_u32<kSc1>(p) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (ld_u32<kSc1>(st) != 0u) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s of the 100 MHz clock
+            __hip_atomic_fetch_or((gu32*)st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+// every wave drains its stores, then thread 0 publishes the item
+__device__ __forceinline__ void flow_signal(uint32_t* p) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct FlowItem {
+    int kind;   // 0 PC unit, 1 MTD tile, 2 range-only, -1 nothing (the PC of a CPI past the last)
+    int j;      // the CPI's index in its queue
+    int idx;    // unit / tile / region
+};
+
+__device__ __forceinline__ int flow_cpis(int ncpi, int q) {
+    return ncpi > q ? (ncpi - q + kFlowQueues - 1) / kFlowQueues : 0;
+}
+__device__ __forceinline__ uint32_t flow_total(const FlowArgs& a, int q, int nh) {
+    const int J = flow_cpis(a.ncpi, q);
+    const int npc = a.nl + a.nsh;
+    return J > 0 ? (uint32_t)npc + (uint32_t)J * (uint32_t)(npc + a.nm) + (uint32_t)nh : 0u;
+}
+__device__ __forceinline__ FlowItem flow_decode(const FlowArgs& a, int q, int nh, uint32_t k) {
+    const int J = flow_cpis(a.ncpi, q);
+    const uint32_t npc = (uint32_t)(a.nl + a.nsh), T = npc + (uint32_t)a.nm;
+    if (k < npc) return FlowItem{0, 0, (int)k};
+    k -= npc;
+    const uint32_t b = k / T, o = k % T;
+    if (b < (uint32_t)J) {
+        bool pc;
+        uint32_t i;
+        if (a.order == 2) {   // PC(b+1) and MTD(b) dealt evenly through the block
+            const uint32_t p0 = o * npc / T, p1 = (o + 1) * npc / T;
+            pc = p1 > p0;
+            i = pc ? p0 : o - p0;
+        } else {
+            pc = o < npc;
+            i = pc ? o : o - npc;
+        }
+        if (pc) return (int)b + 1 < J ? FlowItem{0, (int)b + 1, (int)i} : FlowItem{-1, 0, 0};
+        return FlowItem{1, (int)b, (int)i};
+    }
+    k -= (uint32_t)J * T;
+    return k < (uint32_t)nh ? FlowItem{2, J - 1, (int)k} : FlowItem{-1, 0, 0};
+}
+
+template <typename TIn, int N1, int N2, int P, int REF>
+__device__ __forceinline__ void flow_item(const FlowArgs& a, int q, const FlowItem& it, int nh, unsigned char* smem,
+                                          uint32_t* s_hits) {
+    using PC = PairCfg<N1, N2>;
+    constexpr int S = kFlowSlots;
+    const int j = it.j, c = q + kFlowQueues * j, slot = j % S;
+    const uint32_t gen = (uint32_t)(j / S);
+    uint32_t* st = flow_status(a.ctl);
+    const size_t R = (size_t)a.a2.R, Ro = (size_t)a.a2.R_out;
+    const size_t plane = (size_t)P * Ro;
+    const int npc = a.nl + a.nsh;
+    const bool hits_on = nh > 0;
+    auto rdm_of = [&](int jj) {
+        return a.rdm_ring ? a.rdm + (size_t)(q * S + jj % S) * plane : a.rdm + (size_t)(q + kFlowQueues * jj) * plane;
+    };
+    auto src_of = [&](int jj) {   // the range stage's view of CPI jj of this queue
+        const int ss = jj % S;
+        return RangeSrc{rdm_of(jj), a.flag ? a.flag + (size_t)(q + kFlowQueues * jj) * plane : nullptr,
+                        a.hring + (size_t)(q * S + ss) * a.nm * a.region, a.hcount + (size_t)(q * S + ss) * a.nm,
+                        a.region, a.cr};
+    };
+    if (it.kind == 0) {   // one PC unit: a long-segment row (sub-block), or RPB1 short-segment rows
+        if (threadIdx.x == 0 && j >= S) flow_wait(flow_ctr(a.ctl, q, slot, 1), gen * (uint32_t)a.nm, st);
+        __syncthreads();
+        const TIn* ein = (const TIn*)a.echo + (size_t)c * P * R;
+        float2* pcs = a.ring + (size_t)(q * S + slot) * P * Ro;
+        float2* lds = reinterpret_cast<float2*>(smem);
+        if (it.idx < a.nl) {
+            constexpr int G = PcCfg<N2>::G;
+            const int ns = a.a2.nsub > 1 ? a.a2.nsub : 1;
+            pc_row<TIn, N2, G, kSc1, G == 64>(ein, pcs, a.a2, it.idx / ns, (int)threadIdx.x % G, lds, it.idx % ns);
+        } else {
+            constexpr int G = PcCfg<N1>::G;
+            const int grp = threadIdx.x / G, ns = a.a1.nsub > 1 ? a.a1.nsub : 1;
+            const int u = (it.idx - a.nl) * PC::RPB1 + grp;
+            pc_row<TIn, N1, G, kSc1, G == 64>(ein, pcs, a.a1, u / ns, (int)threadIdx.x % G, lds + grp * PcCfg<N1>::SLOT,
+                                             u % ns);
+        }
+        flow_signal(flow_ctr(a.ctl, q, slot, 0));
+    } else if (it.kind == 1) {   // one MTD tile (+ Doppler CFAR, hit list) + the range job of CPI j-1
+        if (threadIdx.x == 0) {
+            flow_wait(flow_ctr(a.ctl, q, slot, 0), (gen + 1) * (uint32_t)npc, st);
+            if (hits_on && j >= 1) flow_wait(flow_ctr(a.ctl, q, (j - 1) % S, 1), (uint32_t)((j - 1) / S + 1) * a.nm, st);
+            if (j >= S) flow_wait(flow_ctr(a.ctl, q, (j - S + 1) % S, 1), (uint32_t)((j - S + 1) / S + 1) * a.nm, st);
+        }
+        __syncthreads();
+        MtdTile T;
+        T.pc = a.ring + (size_t)(q * S + slot) * P * Ro;
+        T.rdm = rdm_of(j);
+        T.diff = nullptr;
+        T.flagV = a.flagV ? a.flagV + (size_t)c * plane : nullptr;
+        T.flag = a.flag ? a.flag + (size_t)c * plane : nullptr;
+        T.hits = hits_on ? a.hring + ((size_t)(q * S + slot) * a.nm + it.idx) * a.region : nullptr;
+        T.hit_count = hits_on ? a.hcount + (size_t)(q * S + slot) * a.nm + it.idx : nullptr;
+        T.cell_base = 0;
+        T.bx = it.idx;
+        // one tile instance: a tile without a job runs the hook with n == 0 (its gathers all out of
+        // range), so the kernel carries the MTD code once
+        const RangeSrc rs = src_of(j >= 1 ? j - 1 : j);
+        RangeJob57T<kSc1> rj;
+        const bool job = hits_on && j >= 1;
+        if (job) rj.fetch_idx(rs, it.idx);
+        mtd_tile<P, REF, 1, kSc1, kSc1>(T, a.m, smem, s_hits, RangeHookT<kSc1>{rj, rs});
+        if (job) {
+            rj.finish(rs);
+            if (rj.n > blockDim.x)
+                cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, it.idx, a.region, a.cr,
+                                            (int)(threadIdx.x + blockDim.x), (int)blockDim.x);
+        }
+        flow_signal(flow_ctr(a.ctl, q, slot, 1));
+    } else if (it.kind == 2) {   // the last CPI's range stage: one hit region
+        if (threadIdx.x == 0) flow_wait(flow_ctr(a.ctl, q, slot, 1), (gen + 1) * (uint32_t)a.nm, st);
+        __syncthreads();
+        const RangeSrc rs = src_of(j);
+        cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, it.idx, a.region, a.cr, (int)threadIdx.x,
+                                    (int)blockDim.x);
+    }
+}
+
+template <typename TIn, int N1, int N2, int P, int REF>
+__global__ __launch_bounds__(kBlock, 4) void flow_kernel(FlowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_item, s_hits;
+    const int nh = (a.flag && a.cr.rflag && a.m.cv.enabled) ? a.nm : 0;
+    int h = (int)xcc_id();
+    if (threadIdx.x == 0)
+        s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
+    int tried = 1;
+    for (;;) {
+        __syncthreads();   // every thread has read s_item
+        if (k >= flow_total(a, h, nh)) {   // this queue is drained: help the next one
+            if (tried == kFlowQueues) break;
+            ++tried;
+            h = (h + 1) % kFlowQueues;
+            if (threadIdx.x == 0)
+                s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
+            continue;
+        }
+        uint32_t nxt = 0;
+        if (threadIdx.x == 0)   // claim ahead: the atomic's latency hides under the item
+            nxt = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // The item reads its arguments through an opaque copy of the kernarg pointer: otherwise
+        // hipcc hoists every field any item type uses into SGPRs for the whole loop (hundreds of
+        // SGPR spills into VGPR lanes, then VGPR spills).  The pointer stays constant-address-space,
+        // so the re-reads are scalar loads.
+        typedef const __attribute__((address_space(4))) FlowArgs FlowArgsK;
+        const FlowArgsK* ap = (const FlowArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        const FlowArgs& ai = *(const FlowArgs*)ap;
+        const FlowItem it = flow_decode(ai, h, nh, k);
+        flow_item<TIn, N1, N2, P, REF>(ai, h, it, nh, smem, &s_hits);
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = nxt;
+        __syncthreads();
+        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
+    }
+}
+
+template <typename TIn, int N1, int N2, int P, int REF>
+static hipError_t launch_flow_t(FlowArgs& a, hipStream_t s) {
+    using PC = PairCfg<N1, N2>;
+    using MC = MtdCfg<P>;
+    static_assert(PC::T == kBlock && MC::T == kBlock, "flow items are 256-thread workgroups");
+    constexpr size_t lds = PC::lds > MC::template lds_for<REF>() ? PC::lds : MC::template lds_for<REF>();
+    static LaunchOnce once;
+    int resident = 0;
+    hipError_t e = launch_once(once, &resident, [&](int dev, int* v) {
+        hipError_t r = hipFuncSetAttribute((const void*)flow_kernel<TIn, N1, N2, P, REF>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (r != hipSuccess) return r;
+        int per = 0, cus = 0;
+        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)flow_kernel<TIn, N1, N2, P, REF>, kBlock,
+                                                         lds);
+        if (r != hipSuccess) return r;
+        r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        *v = per * cus;
+        return r;
+    });
+    if (e != hipSuccess) return e;
+    if (resident < 1) return hipErrorLaunchOutOfResources;
+    const int ns2 = a.a2.nsub > 1 ? a.a2.nsub : 1, ns1 = a.a1.nsub > 1 ? a.a1.nsub : 1;
+    a.nl = P * ns2;
+    a.nsh = (P * ns1 + PC::RPB1 - 1) / PC::RPB1;
+    a.nm = (a.a2.R_out + MC::W - 1) / MC::W;
+    a.region = MC::W * P;
+    const int64_t items = (int64_t)a.ncpi * (a.nl + a.nsh + a.nm) + (int64_t)kFlowQueues * (a.nl + a.nsh + a.nm);
+    const int grid = items < resident ? (int)items : resident;
+    hipLaunchKernelGGL((flow_kernel<TIn, N1, N2, P, REF>), dim3((unsigned)grid), dim3(kBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams) {
+    return beams == 1 && P == 128 && nfft1 == 1024 && nfft2 == 4096 && (dtype == RSP_C64 || dtype == RSP_C32F16);
+}
+
+hipError_t launch_flow(FlowArgs& a, int dtype, hipStream_t s) {
+    if (a.ncpi <= 0) return hipSuccess;
+    if (!flow_supported(a.m.P, a.a1.mf.nfft, a.a2.mf.nfft, dtype, a.m.beams)) return hipErrorNotSupported;
+    if (a.m.cv.enabled && !(a.m.cv.ref == 5 && a.m.cv.save == 7)) return hipErrorNotSupported;
+    if (a.m.cv.enabled && a.cr.rflag && !(a.cr.ref == 5 && a.cr.save == 7)) return hipErrorNotSupported;
+    if (dtype == RSP_C64) return launch_flow_t<float2, 1024, 4096, 128, 5>(a, s);
+    return launch_flow_t<__half2, 1024, 4096, 128, 5>(a, s);
 }
 
 // ================================================================== Doppler CFAR from an RDM

@@ -30,9 +30,10 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
            "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_set_host_pipeline", "rsp_ingest_record_bytes",
-           "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter")
-RSP_NKERNELS = 4
-KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
+           "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter",
+           "rsp_set_flow", "rsp_flow_status")
+RSP_NKERNELS = 5
+KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "flow_kernel")
 
 
 class RspError(RuntimeError):
@@ -108,6 +109,10 @@ def load_library(path=None):
     lib.rsp_destroy.argtypes = [vp]
     lib.rsp_set_chunk.restype = C.c_int
     lib.rsp_set_chunk.argtypes = [vp, i64]
+    lib.rsp_set_flow.restype = C.c_int
+    lib.rsp_set_flow.argtypes = [vp, C.c_int32]
+    lib.rsp_flow_status.restype = C.c_int
+    lib.rsp_flow_status.argtypes = [vp, C.POINTER(C.c_int32)]
     lib.rsp_pc_mtd.restype = C.c_int
     lib.rsp_pc_mtd.argtypes = [vp, vp, i32, i32, i64, i64, i64, vp, i32]
     lib.rsp_cfar.restype = C.c_int

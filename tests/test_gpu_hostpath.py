@@ -87,3 +87,37 @@ def test_host_path_repeated_calls_and_fp16(torch_cuda):
     got = eng.pc_mtd_cfar(iq, cf, want_flagV=False)
     assert np.array_equal(got[0], rdm.cpu().numpy()) and np.array_equal(got[1], flag.cpu().numpy())
     eng.close()
+
+
+@pytest.mark.parametrize("chunk", [1, 2])
+def test_host_path_two_beam_dmx(torch_cuda, chunk):
+    """A two-beam (DMX) context through the host pipeline: in_cpi / dev_cpi scale by the beams
+    and the column-major ingest converts batch * beams planes.  MATLAB's layout (C128, P x R
+    column-major per beam), chunks smaller than the batch: bit-exact against the device path on
+    the same complex64 samples."""
+    torch = torch_cuda
+    from rsp import _capi as capi
+    from rsp import presets
+    from rsp.engine import Engine
+    spec = presets.dmx_native()
+    eng = Engine(spec, device=0)
+    cf = presets.dmx_native_cfar(spec)
+    B = 3
+    rng = np.random.default_rng(4040 + chunk)
+    e = ((rng.standard_normal((B, 2, spec.P, spec.R)) + 1j * rng.standard_normal((B, 2, spec.P, spec.R)))
+         * np.sqrt(0.5)).astype(np.complex64)
+    V, Ro = eng.shape
+    rdm = torch.empty((B, V, Ro), dtype=torch.float32, device="cuda")
+    flag = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+    fv = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+    eng.run_dev(torch.from_numpy(e).cuda(), rdm=rdm, flag=flag, flagV=fv, cfar=cf)
+    torch.cuda.synchronize()
+    want = (rdm.cpu().numpy(), flag.cpu().numpy(), fv.cpu().numpy())
+    eng.set_host_pipeline(chunk, 0)
+    col = np.ascontiguousarray(np.swapaxes(e.astype(np.complex128), 2, 3))   # [B, beams, R, P]
+    got = eng.pc_mtd_cfar(col, cf, layout=capi.RSP_COLMAJOR)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    rdm2, flag2, _ = eng.pc_mtd_cfar(e, cf, want_flagV=False)   # row-major complex64
+    assert np.array_equal(rdm2, want[0]) and np.array_equal(flag2, want[1])
+    eng.close()
