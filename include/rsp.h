@@ -209,6 +209,21 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
                     float* rdm_out /* nullable */, int32_t out_layout, uint8_t* flag_out,
                     uint8_t* flagV_out /* nullable */);
 
+/* MATLAB-typed forms for the MEX drop-ins (replacing the .m functions' own double outputs,
+ * MTD/fun_MTD_produce.m:12 and CFAR_WangCai/executeCFAR.m:1-2): as rsp_pc_mtd_cfar / rsp_cfar,
+ * but the RDM and the 0/1 flags land as double and the CFAR input is double.  The widening
+ * (float -> double, byte -> double) and narrowing (double -> float, round to nearest) run on
+ * the host copy threads, piece by piece as each pinned piece's DMA lands, instead of in a
+ * serial loop in the shim.  Values are identical to the float / byte forms'.  rsp_pc_mtd_cfar_f64
+ * with cfar == NULL is fun_MTD_produce. */
+int rsp_pc_mtd_cfar_f64(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,
+                        int64_t P, int64_t R, int64_t batch, const rsp_cfar_params* cfar,
+                        double* rdm_out /* nullable */, int32_t out_layout, double* flag_out,
+                        double* flagV_out /* nullable */);
+int rsp_cfar_f64(rsp_ctx* ctx, const double* rdm, int32_t rdm_layout, int64_t V, int64_t R,
+                 int64_t batch, const rsp_cfar_params* cfar, double* flag_out,
+                 double* flagV_out /* nullable */);
+
 /* ---- device-pointer entry points, asynchronous on `stream` -------------------------- */
 /* d_echo: [batch][P][R] rsp_dtype RSP_C64 or RSP_C32F16.  cfar == NULL: PC + MTD only.
  * d_rdm may be NULL only when cfar != NULL (then an internal buffer is used). */
@@ -396,7 +411,7 @@ int rsp_set_prefilter(rsp_ctx* ctx, const float* gain /* nullable, host [R] */, 
  * built for the v2 c2/c3 shape (128 pulses, 1024 + 4096-point matched filters, one beam, CFAR
  * with the reference's 5 + 7 windows or none, no fused pre-filter); other contexts and calls
  * keep mode 0 whatever is set. */
-int rsp_set_flow(rsp_ctx* ctx, int32_t mode);
+int rsp_set_flow(rsp_ctx* ctx, int32_t mode);   /* (mode + 4 * lead + 16 * lag: dev tuning bits, see rsp_capi.cpp) */
 /* After a dataflow call: *timed_out = 1 if a hand-off wait of the last launch exceeded its
  * bound (0.5 s) -- the launch then finished with unspecified outputs instead of hanging.
  * Synchronises the device. */

@@ -725,7 +725,11 @@ static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSu
 
 int rsp_set_flow(rsp_ctx* ctx, int32_t mode) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_flow: null ctx");
-    if (mode < 0 || mode > 2) return fail(ctx, RSP_ERR_ARG, "rsp_set_flow: mode must be 0..2");
+    // mode bits: 0-1 order (0 off, 1 blocked, 2 interleaved); 2-3 PC lead, 4-5 range-job lag (0 = the
+    // default 2; 1 or 2): tuning for A/B runs
+    const int order = mode & 3, lead = (mode >> 2) & 3, lag = (mode >> 4) & 3;
+    if (mode < 0 || mode > 63 || order == 3 || lead == 3 || lag == 3 || (order == 0 && mode != 0))
+        return fail(ctx, RSP_ERR_ARG, "rsp_set_flow: bad mode %d", mode);
     ctx->flow = mode;
     return RSP_OK;
 }
@@ -1010,7 +1014,9 @@ static int run_flow(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncp
     f.flagV = cfar ? d_flagV : nullptr;
     f.ctl = (uint32_t*)ctx->fl_ctl.p;
     f.ncpi = (int)ncpi;
-    f.order = ctx->flow;
+    f.order = ctx->flow & 3;
+    f.lead = (ctx->flow >> 2) & 3 ? (ctx->flow >> 2) & 3 : 2;
+    f.lag = (ctx->flow >> 4) & 3 ? (ctx->flow >> 4) & 3 : 2;
     HIP_TRY(ctx, hipMemsetAsync(ctx->fl_ctl.p, 0, ctx->fl_ctl.n, s));
     HIP_TRY(ctx, timed(ctx, RSP_K_FLOW, s, [&] { return rsp::launch_flow(f, dtype, s); }));
     return RSP_OK;
@@ -1529,7 +1535,8 @@ static size_t piece_for(const rsp_ctx* ctx, size_t bytes) {
 
 // `bytes` = the device-side bytes; narrow: src is complex double, narrowed to complex float on
 // the way into the pinned piece (half the PCIe bytes of MATLAB's C128 echo).
-static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes, bool narrow = false) {
+// narrow 2: src is real double, narrowed to float the same way (rsp_cfar_f64).
+static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes, int narrow = 0) {
     auto& h = ctx->hp;
     rsp::CopyPool& pool = host_pool(ctx);
     const size_t piece = piece_for(ctx, bytes);
@@ -1538,7 +1545,9 @@ static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes, bool
         const int r = h.ring_in;
         h.ring_in = (h.ring_in + 1) % h.kRing;
         HIP_TRY(ctx, hipEventSynchronize(h.ev_pin_in[r]));   // the slot's previous DMA is done
-        if (narrow)
+        if (narrow == 2)
+            pool.narrow_f64((float*)h.pin_in[r], (const double*)((const char*)src + 2 * off), n / 4);
+        else if (narrow)
             pool.narrow_c128((float*)h.pin_in[r], (const double*)((const char*)src + 2 * off), n / 8);
         else
             pool.copy(h.pin_in[r], (const char*)src + off, n);
@@ -1550,10 +1559,13 @@ static int h2d_pieces(rsp_ctx* ctx, void* d, const void* src, size_t bytes, bool
 
 // device -> host (pageable), through the pinned output ring on the D2H stream: up to kRing
 // pieces in flight; each is copied out by the pool once its DMA is done.
+// widen: the host side takes MATLAB's double -- 1: float cells, 2: 0/1 bytes -- converted by the
+// pool as each pinned piece lands (bytes = device-side bytes; the host array is 8 bytes per element)
 struct D2HPart {
     const void* d;
     void* h;
     size_t bytes;
+    int widen = 0;
 };
 static int d2h_pieces(rsp_ctx* ctx, const std::vector<D2HPart>& parts) {
     auto& h = ctx->hp;
@@ -1562,12 +1574,15 @@ static int d2h_pieces(rsp_ctx* ctx, const std::vector<D2HPart>& parts) {
         const char* d;
         char* h;
         size_t n;
+        int widen;
     };
     std::vector<Piece> ps;
     for (const D2HPart& p : parts) {
         const size_t piece = piece_for(ctx, p.bytes);
+        const size_t scale = p.widen == 1 ? 2 : (p.widen == 2 ? 8 : 1);   // host bytes per device byte
         for (size_t off = 0; off < p.bytes; off += piece)
-            ps.push_back({(const char*)p.d + off, (char*)p.h + off, p.bytes - off < piece ? p.bytes - off : piece});
+            ps.push_back({(const char*)p.d + off, (char*)p.h + off * scale, p.bytes - off < piece ? p.bytes - off : piece,
+                          p.widen});
     }
     const size_t np = ps.size();
     auto issue = [&](size_t i) -> int {
@@ -1582,7 +1597,9 @@ static int d2h_pieces(rsp_ctx* ctx, const std::vector<D2HPart>& parts) {
     for (size_t i = 0; i < np; ++i) {
         const int r = (int)(i % h.kRing);
         HIP_TRY(ctx, hipEventSynchronize(h.ev_pin_out[r]));
-        pool.copy(ps[i].h, h.pin_out[r], ps[i].n);
+        if (ps[i].widen == 1) pool.widen_f32((double*)ps[i].h, (const float*)h.pin_out[r], ps[i].n / 4);
+        else if (ps[i].widen == 2) pool.widen_u8((double*)ps[i].h, (const uint8_t*)h.pin_out[r], ps[i].n);
+        else pool.copy(ps[i].h, h.pin_out[r], ps[i].n);
         if (i + h.kRing < np && (rc = issue(i + h.kRing))) return rc;
     }
     return RSP_OK;
@@ -1599,16 +1616,17 @@ int rsp_set_host_pipeline(rsp_ctx* ctx, int64_t cpis_per_chunk, int32_t copy_thr
 }
 
 static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
-                      int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
-                      uint8_t* flag_out, uint8_t* flagV_out);
+                      int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout,
+                      void* flag_out, void* flagV_out, bool f64);
 
-int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
-                    int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
-                    uint8_t* flag_out, uint8_t* flagV_out) {
+// The host-buffer chain: float / byte outputs, or (f64) MATLAB's double outputs.
+static int host_call(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                     int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout, void* flag_out,
+                     void* flagV_out, bool f64) {
     if (!ctx) return fail(nullptr, RSP_ERR_ARG, "null ctx");
     int rc;
     try {
-        rc = host_chain(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out);
+        rc = host_chain(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out, f64);
     } catch (const std::bad_alloc&) {
         rc = fail(ctx, RSP_ERR_NOMEM, "rsp_pc_mtd_cfar: host allocation failed");
     } catch (const std::exception& e) {
@@ -1627,9 +1645,21 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
     return rc;
 }
 
+int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                    int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
+                    uint8_t* flag_out, uint8_t* flagV_out) {
+    return host_call(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out, false);
+}
+
+int rsp_pc_mtd_cfar_f64(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                        int64_t batch, const rsp_cfar_params* cfar, double* rdm_out, int32_t out_layout,
+                        double* flag_out, double* flagV_out) {
+    return host_call(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out, true);
+}
+
 static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
-                      int64_t batch, const rsp_cfar_params* cfar, float* rdm_out, int32_t out_layout,
-                      uint8_t* flag_out, uint8_t* flagV_out) {
+                      int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout,
+                      void* flag_out, void* flagV_out, bool f64) {
     int rc = check_host_call(ctx, echo, dtype, layout, P, R, batch);
     if (rc) return rc;
     if (out_layout != RSP_ROWMAJOR && out_layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad out_layout");
@@ -1703,9 +1733,12 @@ static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t lay
         const size_t n = (size_t)chunk_n(k), o = (size_t)k * K * cells;
         HIP_TRY(ctx, hipStreamWaitEvent(h.s_d2h, h.ev_comp[sl], 0));
         std::vector<D2HPart> parts;
-        if (rdm_out) parts.push_back({tr ? h.tr[sl][0].p : h.rdm[sl].p, rdm_out + o, n * cells * sizeof(float)});
-        if (cfar) parts.push_back({tr ? h.tr[sl][1].p : h.flag[sl].p, flag_out + o, n * cells});
-        if (want_fv) parts.push_back({tr ? h.tr[sl][2].p : h.flagV[sl].p, flagV_out + o, n * cells});
+        const size_t rb = f64 ? 8 : 4, fb = f64 ? 8 : 1;   // host bytes per RDM / flag element
+        if (rdm_out)
+            parts.push_back({tr ? h.tr[sl][0].p : h.rdm[sl].p, (char*)rdm_out + o * rb, n * cells * sizeof(float), f64 ? 1 : 0});
+        if (cfar) parts.push_back({tr ? h.tr[sl][1].p : h.flag[sl].p, (char*)flag_out + o * fb, n * cells, f64 ? 2 : 0});
+        if (want_fv)
+            parts.push_back({tr ? h.tr[sl][2].p : h.flagV[sl].p, (char*)flagV_out + o * fb, n * cells, f64 ? 2 : 0});
         int rc2 = d2h_pieces(ctx, parts);
         if (rc2) return rc2;
         HIP_TRY(ctx, hipEventRecord(h.ev_out[sl], h.s_d2h));
@@ -1716,7 +1749,7 @@ static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t lay
         // the slot's previous chain (chunk k-2) has read its input
         if (k >= h.kSlots) HIP_TRY(ctx, hipStreamWaitEvent(h.s_h2d, h.ev_comp[sl], 0));
         if ((rc = h2d_pieces(ctx, h.in[sl].p, (const char*)echo + (size_t)k * K * in_cpi, (size_t)chunk_n(k) * dev_cpi,
-                             narrow)))
+                             narrow ? 1 : 0)))
             return rc;
         HIP_TRY(ctx, hipEventRecord(h.ev_in[sl], h.s_h2d));
         if ((rc = compute(k))) return rc;
@@ -1759,5 +1792,73 @@ int rsp_cfar(rsp_ctx* ctx, const float* rdm, int32_t rdm_layout, int64_t V, int6
     if (flagV_out && (rc = fetch(ctx, (const uint8_t*)ctx->st_flagV.p, flagV_out, batch, V, R, rdm_layout)))
         return rc;
     return RSP_OK;
+}
+
+// executeCFAR with MATLAB's types (rsp.h): the double RDM narrowed to float by the copy pool on
+// its way into the pinned input ring, the 0/1 flags widened to double as their pieces land.
+static int cfar_f64_body(rsp_ctx* ctx, const double* rdm, int32_t rdm_layout, int64_t V, int64_t R, int64_t batch,
+                         const rsp_cfar_params* cfar, double* flag_out, double* flagV_out) {
+    int rc;
+    if ((rc = host_pipe_init(ctx))) return rc;
+    const size_t cells = (size_t)batch * V * R;
+    if ((rc = ensure(ctx, ctx->st_in, cells * sizeof(float)))) return rc;
+    if ((rc = ensure(ctx, ctx->st_rdm, cells * sizeof(float)))) return rc;
+    if ((rc = ensure(ctx, ctx->st_flag, cells))) return rc;
+    if ((rc = ensure(ctx, ctx->st_flagV, cells))) return rc;
+    auto& h = ctx->hp;
+    if ((rc = h2d_pieces(ctx, ctx->st_in.p, rdm, cells * sizeof(float), 2))) return rc;
+    HIP_TRY(ctx, hipEventRecord(h.ev_in[0], h.s_h2d));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_in[0], 0));
+    const float* d_rdm = (const float*)ctx->st_in.p;
+    const bool col = rdm_layout == RSP_COLMAJOR;
+    if (col) {  // MATLAB V x R = [b][R][V] -> [b][V][R]
+        HIP_TRY(ctx, rsp::launch_transpose_f32(d_rdm, (float*)ctx->st_rdm.p, batch, (int)R, (int)V, ctx->stream));
+        d_rdm = (const float*)ctx->st_rdm.p;
+    }
+    rc = rsp_cfar_dev(ctx, d_rdm, V, R, batch, cfar, (uint8_t*)ctx->st_flag.p, (uint8_t*)ctx->st_flagV.p, ctx->stream);
+    if (rc) return rc;
+    const uint8_t* f = (const uint8_t*)ctx->st_flag.p;
+    const uint8_t* fv = (const uint8_t*)ctx->st_flagV.p;
+    if (col) {   // back to MATLAB's [b][R][V]
+        if ((rc = ensure(ctx, ctx->st_t, cells))) return rc;
+        if ((rc = ensure(ctx, ctx->st_canon, cells))) return rc;
+        HIP_TRY(ctx, rsp::launch_transpose_u8(f, (uint8_t*)ctx->st_t.p, batch, (int)V, (int)R, ctx->stream));
+        f = (const uint8_t*)ctx->st_t.p;
+        if (flagV_out) {
+            HIP_TRY(ctx, rsp::launch_transpose_u8(fv, (uint8_t*)ctx->st_canon.p, batch, (int)V, (int)R, ctx->stream));
+            fv = (const uint8_t*)ctx->st_canon.p;
+        }
+    }
+    HIP_TRY(ctx, hipEventRecord(h.ev_comp[0], ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(h.s_d2h, h.ev_comp[0], 0));
+    std::vector<D2HPart> parts;
+    parts.push_back({f, flag_out, cells, 2});
+    if (flagV_out) parts.push_back({fv, flagV_out, cells, 2});
+    if ((rc = d2h_pieces(ctx, parts))) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(h.s_d2h));
+    return RSP_OK;
+}
+
+int rsp_cfar_f64(rsp_ctx* ctx, const double* rdm, int32_t rdm_layout, int64_t V, int64_t R, int64_t batch,
+                 const rsp_cfar_params* cfar, double* flag_out, double* flagV_out) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "null ctx");
+    if (!rdm || !cfar || !flag_out || V < 1 || R < 1 || batch < 0) return fail(ctx, RSP_ERR_ARG, "rsp_cfar_f64: bad argument");
+    if (rdm_layout != RSP_ROWMAJOR && rdm_layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad rdm_layout");
+    if (batch == 0) return RSP_OK;
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    int rc;
+    try {
+        rc = cfar_f64_body(ctx, rdm, rdm_layout, V, R, batch, cfar, flag_out, flagV_out);
+    } catch (const std::exception& e) {
+        rc = fail(ctx, RSP_ERR_NOMEM, "rsp_cfar_f64: host pipeline: %s", e.what());
+    } catch (...) {
+        rc = fail(ctx, RSP_ERR_NOMEM, "rsp_cfar_f64: host pipeline: unknown exception");
+    }
+    if (rc && ctx->hp.s_h2d) {
+        (void)hipStreamSynchronize(ctx->hp.s_h2d);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->hp.s_d2h);
+    }
+    return rc;
 }
 

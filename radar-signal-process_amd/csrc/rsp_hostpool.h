@@ -5,6 +5,7 @@
 // per direction, so each staging piece is split over the pool.
 #pragma once
 #include <condition_variable>
+#include <cstdint>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -43,6 +44,24 @@ public:
     void narrow_c128(float* dst, const double* src, size_t n) {
         run(n, 512, [=](size_t a, size_t b) {
             for (size_t i = 2 * a; i < 2 * b; ++i) dst[i] = (float)src[i];
+        });
+    }
+
+    // MATLAB's output types: float RDM cells and 0/1 flag bytes widened to double (exact), and
+    // a real double input narrowed to float (round to nearest, as the (float) cast on the GPU)
+    void widen_f32(double* dst, const float* src, size_t n) {
+        run(n, 1024, [=](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i) dst[i] = (double)src[i];
+        });
+    }
+    void narrow_f64(float* dst, const double* src, size_t n) {
+        run(n, 1024, [=](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i) dst[i] = (float)src[i];
+        });
+    }
+    void widen_u8(double* dst, const uint8_t* src, size_t n) {
+        run(n, 4096, [=](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i) dst[i] = (double)src[i];
         });
     }
 

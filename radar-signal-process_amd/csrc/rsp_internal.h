@@ -154,7 +154,7 @@ struct MtdArgs {
 // ring of kFlowSlots scratch slots per queue; hand-offs between workgroups are write-through
 // (sc1 stores, drained, one counter add per item) and read with sc1 loads.
 constexpr int kFlowQueues = 8;
-constexpr int kFlowSlots = 3;
+constexpr int kFlowSlots = 4;   // >= lead + 2 and >= lag + 2 (FlowArgs)
 constexpr int kFlowLine = 32;   // uint32 per control line (128 B)
 // control words: heads [kFlowQueues], counters [kFlowQueues][kFlowSlots][2] (PC units, MTD
 // tiles done), then the status line (a wait that timed out)
@@ -175,7 +175,9 @@ struct FlowArgs {
     int ncpi;
     int nl, nsh, nm;       // per CPI: long-row units, short-row groups, MTD tiles
     int region;            // hit-list entries per tile
-    int order;             // 1: a CPI's MTD tiles after the next CPI's PC units; 2: the two interleaved
+    int order;             // 1: a block's PC units first, then its MTD tiles; 2: the two interleaved
+    int lead;              // block b holds the MTD tiles of CPI b and the PC units of CPI b + lead (1, 2)
+    int lag;               // the MTD tiles of CPI j carry the range jobs of CPI j - lag (1, 2)
 };
 bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams);
 hipError_t launch_flow(FlowArgs& a, int dtype, hipStream_t s);

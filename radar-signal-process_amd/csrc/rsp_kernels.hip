@@ -323,7 +323,7 @@ __device__ __forceinline__ void pc_dma_read(float2 (&u)[N / G], float2* slot, in
 // SGPRs -- the zero padding beyond in_len, the out_len cut and invalid rows (num_records 0)
 // are the hardware range check, with no per-element branch.  G < 64 (N <= 512): rows share
 // a wave, so the accesses stay per-lane predicated.
-template <typename TIn, int N, int G, int SA = 0, bool WS = false>
+template <typename TIn, int N, int G, int SA = 0, bool WS = false, int EARLY = -1>
 __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __restrict__ out,
                                        const PcMfArgs& a, int row, int t, float2* buf, int sub = 0) {
     constexpr int E = N / G;
@@ -334,7 +334,9 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     // paired kernel's allocation, which its short-row path already sets; PC 41 -> 39.8 us per
     // 16 CPIs at c3, 39.7 -> 37.8 us per CPI at c5).  8192/16384-point rows keep the spectrum
     // loads after the forward FFT.
-    constexpr bool kEarly = G <= 64 || N <= 4096;
+    // (EARLY 0 / 1 overrides: the dataflow kernel's long rows load the spectrum late -- its item
+    // loop leaves no room for 32 early spectrum registers)
+    constexpr bool kEarly = EARLY >= 0 ? EARLY != 0 : (G <= 64 || N <= 4096);
     if constexpr (kUniform) {   // (a VGPR-held offset in a buffer resource means a waterfall loop per access)
         row = __builtin_amdgcn_readfirstlane(row);
         sub = __builtin_amdgcn_readfirstlane(sub);
@@ -943,6 +945,16 @@ __device__ __forceinline__ void prev_chunk_hits(const MtdArgs& a, int wg, int nw
 // r+7 .. r+13) right after the tile's own loads,
 // and the test + first-maximum scatter run after the tile -- the three dependent gathers hide
 // under the tile's FFT and Doppler CFAR instead of trailing the workgroup.
+// The thread's index in its workgroup.  OPQ: through an empty volatile asm, so the value (and
+// everything derived from it) is recomputed where it is used instead of being hoisted out of the
+// dataflow kernel's item loop and held -- spilled -- across every item.
+template <bool OPQ>
+__device__ __forceinline__ int tid_of() {
+    int t = (int)threadIdx.x;
+    if constexpr (OPQ) asm volatile("" : "+v"(t));
+    return t;
+}
+
 // Where a range job reads and writes: the previous chunk's RDM / flag planes, hit lists and
 // counts (MtdArgs::prev_* in the chunked pipeline; the dataflow kernel's ring slots otherwise).
 struct RangeSrc {
@@ -1007,7 +1019,7 @@ struct RangeJob57T {
         // both loads issue at once: a region holds W*P >= blockDim entries, so the index load
         // is in bounds (and ignored) past the count -- no count -> index round trip
         n = ld_u32<LA>(s.count + rg);
-        idx = ld_u32<LA>(s.hits + (size_t)rg * s.region + threadIdx.x);
+        idx = ld_u32<LA>(s.hits + (size_t)rg * s.region + tid_of<LA != 0>());
     }
     __device__ __forceinline__ void fetch_cells(const RangeSrc& s) {
         // Every wave of every MTD workgroup issues these 17 loads, unconditionally: a lane
@@ -1016,7 +1028,7 @@ struct RangeJob57T {
         // (vmcnt counts in issue order) merged from two paths, so a wave with hits would wait
         // for its gathers before its first butterfly (c3: 3.8 us per 16-CPI launch).
         const CfarRArgs& c = s.cr;
-        const bool mine = threadIdx.x < n;
+        const bool mine = (uint32_t)tid_of<LA != 0>() < n;
         const uint32_t R = c.R > 0 ? (uint32_t)c.R : 1u, V = c.V > 0 ? (uint32_t)c.V : 1u;   // (no job: unset)
         const uint32_t row = idx / R;
         const int r = (int)(idx - row * R);
@@ -1025,7 +1037,7 @@ struct RangeJob57T {
         gather(x, buf_rsrc(s.rdm, kOob), row, r, mine && !zrow, c.R);   // (job => the RDM is < kOob bytes)
     }
     __device__ __forceinline__ void finish(const RangeSrc& s) {
-        if (threadIdx.x >= n) return;
+        if ((uint32_t)tid_of<LA != 0>() >= n) return;
         const CfarRArgs& c = s.cr;
         const uint32_t row = idx / (uint32_t)c.R;
         const int r = (int)(idx - row * (uint32_t)c.R);
@@ -1062,18 +1074,21 @@ struct NoHook {
 template <int P, int BEAMS, int LA, int W>
 __host__ __device__ constexpr bool kMtdDma() {
 #ifndef RSP_MTD_NO_DMA
-    return BEAMS == 1 && LA == 0 && W >= 2 && W <= 128 && 64 % (W / 2) == 0;
+    // (LA = kSc1, the dataflow kernel: the pieces are sc1 LDS-DMA loads, L1 bypassed like its
+    // register loads)
+    return BEAMS == 1 && (LA == 0 || LA == kSc1) && W >= 2 && W <= 128 && 64 % (W / 2) == 0;
 #else
     return false;
 #endif
 }
-template <int P, int W, int T>
-__device__ __forceinline__ void mtd_dma_issue(__amdgpu_buffer_rsrc_t src, uint32_t col0, uint32_t R, unsigned char* smem) {
+template <int P, int W, int T, int LA = 0>
+__device__ __forceinline__ void mtd_dma_issue(__amdgpu_buffer_rsrc_t src, uint32_t col0, uint32_t R, unsigned char* smem,
+                                              int tx) {
     constexpr int LPR = W / 2;                    // lanes per row (16 B = 2 columns each)
     constexpr int BYTES = P * W * 8;
     constexpr int NQ = BYTES / (T * 16);          // DMA instructions per thread
     static_assert(BYTES % (T * 16) == 0 && 64 % LPR == 0, "MTD DMA tiling");
-    const int t = threadIdx.x;
+    const int t = tx;
     const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -1084,7 +1099,7 @@ __device__ __forceinline__ void mtd_dma_issue(__amdgpu_buffer_rsrc_t src, uint32
         // rv == false, so nothing computed from it is stored; a select here made hipcc split
         // every DMA into two exec-masked copies)
         const uint32_t vo = ((uint32_t)row * R + col0 + (uint32_t)cp) * 8u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_void*)(smem + (q * T + wb) * 16), 16, vo, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_void*)(smem + (q * T + wb) * 16), 16, vo, 0, 0, LA);
     }
 }
 
@@ -1139,13 +1154,14 @@ constexpr int kMtdLoadPrio = RSP_MTD_PRIO, kMtdLoadPrioMinP = RSP_MTD_PRIO_MINP;
 // One MTD tile: W range bins x all P pulses.  LA / SA: cache policy of the PC loads and of
 // the RDM stores (kSc1 when another workgroup of the same launch consumes them).
 // after_loads(): called once the tile's first-beam loads are issued (RangeJob57 gathers).
-template <int P, int REF, int BEAMS, int LA, int SA, typename Hook = NoHook>
+template <int P, int REF, int BEAMS, int LA, int SA, typename Hook = NoHook, bool OPQ = false>
 __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, unsigned char* smem, uint32_t* s_hits,
                                          const Hook& after_loads = Hook()) {
     using C = MtdCfg<P, BEAMS>;
     constexpr int G = C::G, E = C::E, W = C::W;
-    if (threadIdx.x == 0) *s_hits = 0u;   // published by the FFT's barriers
-    const int c = threadIdx.x % W, g = threadIdx.x / W;
+    const int tx = tid_of<OPQ>();
+    if (tx == 0) *s_hits = 0u;   // published by the FFT's barriers
+    const int c = tx % W, g = tx / W;
     const uint32_t R = (uint32_t)a.R_out;
     const int r = T.bx * W + c;
     const bool rv = r < (int)R;
@@ -1180,7 +1196,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             float wv[E];
 #pragma unroll
             for (int m = 0; m < E; ++m) wv[m] = a.win[g + G * m];
-            mtd_dma_issue<P, W, C::T>(src, (uint32_t)(T.bx * W), R, smem);
+            mtd_dma_issue<P, W, C::T, LA>(src, (uint32_t)(T.bx * W), R, smem, tx);
             // (a compiler barrier: the range gathers below must issue after every DMA piece, or
             // the counted vmcnt would not cover the pieces -- hipcc interleaved them otherwise)
             asm volatile("" ::: "memory");
@@ -1235,7 +1251,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             typedef int v4i __attribute__((ext_vector_type(4)));
             const auto fz = buf_rsrc(T.flag, plane);
             constexpr int SEG = W / 16;
-            for (int i = threadIdx.x; i < P * SEG; i += C::T) {
+            for (int i = tx; i < P * SEG; i += C::T) {
                 const int c0 = T.bx * W + (i % SEG) * 16;
                 if (c0 < (int)R)
                     __builtin_amdgcn_raw_buffer_store_b128(v4i{0, 0, 0, 0}, fz, (uint32_t)(i / SEG) * R + (uint32_t)c0,
@@ -1321,7 +1337,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     RSP_STAMP(1, 4, false);
     if (o.fused && o.rflag) {
         lds_barrier();
-        if (threadIdx.x == 0) {
+        if (tx == 0) {
             if (SA != 0) st_u32_sc1(T.hit_count, *s_hits);
             else *T.hit_count = *s_hits;
         }
@@ -1662,19 +1678,33 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
 // queues.  Resident workgroups claim items from the queue of their own XCD (HW_REG_XCC_ID), so a
 // CPI's PC rows and its MTD tiles normally share one L2, and steal from the other queues once
 // theirs is drained (placement changes speed only: every hand-off is placement-independent).
-// Per queue the item order is PC(0), then for each CPI j: PC(j+1) and MTD(j) (in that order, or
-// interleaved), then the range-only items of the last CPI; every dependency points to an earlier
-// item of the same queue, and items are claimed in queue order by running workgroups, so the
-// smallest unfinished item can always run.
-//   PC unit of CPI j      waits until MTD(j - kFlowSlots) is done with the scratch slot
-//   MTD tile of CPI j     waits for PC(j) (all units), MTD(j-1) (its range job reads that CPI's
-//                         RDM and hit list), MTD(j-kFlowSlots+1) (hit-list / RDM slot reuse)
-//   range-only item       waits for MTD(J-1)
+// Per queue (J CPIs, L = lead, D = lag) the item order is PC(0 .. L-1), then blocks b = 0 .. J-1
+// holding PC(b + L) and MTD(b) (PC first, or interleaved), then range-only items for the last D
+// CPIs.  Every dependency points to an earlier item of the same queue, and items are claimed in
+// queue order by running workgroups, so the smallest unfinished item can always run; the lead
+// and the lag keep each wait a block or more behind the item that satisfies it (a dependency on
+// the previous block waits for its slowest item):
+//   PC unit of CPI j      waits until MTD(j - S) is done with the scratch slot (S = kFlowSlots)
+//   MTD tile of CPI j     waits for PC(j) (all units) and MTD(j - D) (its range job reads that
+//                         CPI's RDM and hit list, written by every tile); slot reuse of the hit
+//                         list / RDM ring needs MTD(j - S + D), implied for S >= D + 2
+//   range-only item       waits for MTD(j) of its CPI
 // Hand-offs follow MI355X_MICROARCH.md's write-through form: every handed-off byte (PC rows, RDM,
 // flag background, hit lists and counts) is stored sc1, every storing wave drains vmcnt before
 // its workgroup's one relaxed counter add, and every load of such bytes is an sc1 load issued
 // after thread 0 saw the counter and the workgroup barrier.  Every wait is bounded (0.5 s; the
 // status word then records it and no later wait blocks), so a protocol fault ends the launch.
+// cache policies of the dataflow kernel's hand-off loads / stores (dev-only -D for timing A/B
+// only: anything but kSc1 breaks the hand-off protocol)
+#ifndef RSP_FLOW_LA
+#define RSP_FLOW_LA kSc1
+#endif
+#ifndef RSP_FLOW_SA
+#define RSP_FLOW_SA kSc1
+#endif
+#ifndef RSP_FLOW_PC_EARLY
+#define RSP_FLOW_PC_EARLY -1   // the long rows' spectrum loads: -1 as pc_row decides, 0 late, 1 early
+#endif
 __device__ __forceinline__ uint32_t xcc_id() {
     uint32_t v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
@@ -1699,12 +1729,14 @@ __device__ __forceinline__ void flow_wait(uint32_t* p, uint32_t target, uint32_t
         }
     }
 }
-// every wave drains its stores, then thread 0 publishes the item
-__device__ __forceinline__ void flow_signal(uint32_t* p) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+
+#ifdef RSP_DIAG_FLOW
+// Dev-only (-DRSP_DIAG_FLOW, tools/diag_flow.py): per workgroup, the first kFlowDiagItems items
+// as {kind | j << 4 | idx << 36, t0 claim decoded, t1 waits done, t2 published} on the 100 MHz
+// clock.
+constexpr int kFlowDiagWG = 1024, kFlowDiagItems = 512;
+__device__ uint64_t g_flow_diag[kFlowDiagWG * kFlowDiagItems * 4];
+#endif
 
 struct FlowItem {
     int kind;   // 0 PC unit, 1 MTD tile, 2 range-only, -1 nothing (the PC of a CPI past the last)
@@ -1717,19 +1749,24 @@ __device__ __forceinline__ int flow_cpis(int ncpi, int q) {
 }
 __device__ __forceinline__ uint32_t flow_total(const FlowArgs& a, int q, int nh) {
     const int J = flow_cpis(a.ncpi, q);
-    const int npc = a.nl + a.nsh;
-    return J > 0 ? (uint32_t)npc + (uint32_t)J * (uint32_t)(npc + a.nm) + (uint32_t)nh : 0u;
+    const uint32_t npc = (uint32_t)(a.nl + a.nsh);
+    return J > 0 ? npc * (uint32_t)a.lead + (uint32_t)J * (npc + (uint32_t)a.nm) + (nh ? (uint32_t)a.lag * nh : 0u)
+                 : 0u;
 }
 __device__ __forceinline__ FlowItem flow_decode(const FlowArgs& a, int q, int nh, uint32_t k) {
     const int J = flow_cpis(a.ncpi, q);
     const uint32_t npc = (uint32_t)(a.nl + a.nsh), T = npc + (uint32_t)a.nm;
-    if (k < npc) return FlowItem{0, 0, (int)k};
-    k -= npc;
+    const uint32_t pro = npc * (uint32_t)a.lead;
+    if (k < pro) {   // the first `lead` CPIs' PC units
+        const int j = (int)(k / npc);
+        return j < J ? FlowItem{0, j, (int)(k % npc)} : FlowItem{-1, 0, 0};
+    }
+    k -= pro;
     const uint32_t b = k / T, o = k % T;
     if (b < (uint32_t)J) {
         bool pc;
         uint32_t i;
-        if (a.order == 2) {   // PC(b+1) and MTD(b) dealt evenly through the block
+        if (a.order == 2) {   // PC(b + lead) and MTD(b) dealt evenly through the block
             const uint32_t p0 = o * npc / T, p1 = (o + 1) * npc / T;
             pc = p1 > p0;
             i = pc ? p0 : o - p0;
@@ -1737,16 +1774,23 @@ __device__ __forceinline__ FlowItem flow_decode(const FlowArgs& a, int q, int nh
             pc = o < npc;
             i = pc ? o : o - npc;
         }
-        if (pc) return (int)b + 1 < J ? FlowItem{0, (int)b + 1, (int)i} : FlowItem{-1, 0, 0};
+        if (pc) return (int)b + a.lead < J ? FlowItem{0, (int)b + a.lead, (int)i} : FlowItem{-1, 0, 0};
         return FlowItem{1, (int)b, (int)i};
     }
     k -= (uint32_t)J * T;
-    return k < (uint32_t)nh ? FlowItem{2, J - 1, (int)k} : FlowItem{-1, 0, 0};
+    if (nh == 0) return FlowItem{-1, 0, 0};
+    const int j = J - a.lag + (int)(k / (uint32_t)nh);   // range-only items of the last `lag` CPIs
+    return j >= 0 && j < J ? FlowItem{2, j, (int)(k % (uint32_t)nh)} : FlowItem{-1, 0, 0};
 }
 
+// The item's waits and body; returns the counter its completion publishes (null: none).  The
+// publishing itself (drain, barrier, counter add) is the caller's, at a fixed point of its loop.
 template <typename TIn, int N1, int N2, int P, int REF>
-__device__ __forceinline__ void flow_item(const FlowArgs& a, int q, const FlowItem& it, int nh, unsigned char* smem,
-                                          uint32_t* s_hits) {
+__device__ __forceinline__ uint32_t* flow_item(const FlowArgs& a, int q, const FlowItem& it, int nh, unsigned char* smem,
+                                               uint32_t* s_hits, uint64_t* diag) {
+    auto stamp = [&](int k) {
+        if (diag && threadIdx.x == 0) diag[k] = __builtin_amdgcn_s_memrealtime();
+    };
     using PC = PairCfg<N1, N2>;
     constexpr int S = kFlowSlots;
     const int j = it.j, c = q + kFlowQueues * j, slot = j % S;
@@ -1768,28 +1812,32 @@ __device__ __forceinline__ void flow_item(const FlowArgs& a, int q, const FlowIt
     if (it.kind == 0) {   // one PC unit: a long-segment row (sub-block), or RPB1 short-segment rows
         if (threadIdx.x == 0 && j >= S) flow_wait(flow_ctr(a.ctl, q, slot, 1), gen * (uint32_t)a.nm, st);
         __syncthreads();
+        stamp(2);
         const TIn* ein = (const TIn*)a.echo + (size_t)c * P * R;
         float2* pcs = a.ring + (size_t)(q * S + slot) * P * Ro;
         float2* lds = reinterpret_cast<float2*>(smem);
         if (it.idx < a.nl) {
             constexpr int G = PcCfg<N2>::G;
             const int ns = a.a2.nsub > 1 ? a.a2.nsub : 1;
-            pc_row<TIn, N2, G, kSc1, G == 64>(ein, pcs, a.a2, it.idx / ns, (int)threadIdx.x % G, lds, it.idx % ns);
+            pc_row<TIn, N2, G, kSc1, G == 64, RSP_FLOW_PC_EARLY>(ein, pcs, a.a2, it.idx / ns, tid_of<true>() % G, lds,
+                                                                 it.idx % ns);
         } else {
             constexpr int G = PcCfg<N1>::G;
-            const int grp = threadIdx.x / G, ns = a.a1.nsub > 1 ? a.a1.nsub : 1;
+            const int tx = tid_of<true>();
+            const int grp = tx / G, ns = a.a1.nsub > 1 ? a.a1.nsub : 1;
             const int u = (it.idx - a.nl) * PC::RPB1 + grp;
-            pc_row<TIn, N1, G, kSc1, G == 64>(ein, pcs, a.a1, u / ns, (int)threadIdx.x % G, lds + grp * PcCfg<N1>::SLOT,
+            pc_row<TIn, N1, G, kSc1, G == 64>(ein, pcs, a.a1, u / ns, tx % G, lds + grp * PcCfg<N1>::SLOT,
                                              u % ns);
         }
-        flow_signal(flow_ctr(a.ctl, q, slot, 0));
+        return flow_ctr(a.ctl, q, slot, 0);
     } else if (it.kind == 1) {   // one MTD tile (+ Doppler CFAR, hit list) + the range job of CPI j-1
+        const int D = a.lag;
         if (threadIdx.x == 0) {
             flow_wait(flow_ctr(a.ctl, q, slot, 0), (gen + 1) * (uint32_t)npc, st);
-            if (hits_on && j >= 1) flow_wait(flow_ctr(a.ctl, q, (j - 1) % S, 1), (uint32_t)((j - 1) / S + 1) * a.nm, st);
-            if (j >= S) flow_wait(flow_ctr(a.ctl, q, (j - S + 1) % S, 1), (uint32_t)((j - S + 1) / S + 1) * a.nm, st);
+            if (hits_on && j >= D) flow_wait(flow_ctr(a.ctl, q, (j - D) % S, 1), (uint32_t)((j - D) / S + 1) * a.nm, st);
         }
         __syncthreads();
+        stamp(2);
         MtdTile T;
         T.pc = a.ring + (size_t)(q * S + slot) * P * Ro;
         T.rdm = rdm_of(j);
@@ -1802,29 +1850,36 @@ __device__ __forceinline__ void flow_item(const FlowArgs& a, int q, const FlowIt
         T.bx = it.idx;
         // one tile instance: a tile without a job runs the hook with n == 0 (its gathers all out of
         // range), so the kernel carries the MTD code once
-        const RangeSrc rs = src_of(j >= 1 ? j - 1 : j);
+        const RangeSrc rs = src_of(j >= D ? j - D : j);
         RangeJob57T<kSc1> rj;
-        const bool job = hits_on && j >= 1;
+        const bool job = hits_on && j >= D;
         if (job) rj.fetch_idx(rs, it.idx);
-        mtd_tile<P, REF, 1, kSc1, kSc1>(T, a.m, smem, s_hits, RangeHookT<kSc1>{rj, rs});
+        mtd_tile<P, REF, 1, RSP_FLOW_LA, RSP_FLOW_SA, RangeHookT<kSc1>, true>(T, a.m, smem, s_hits, RangeHookT<kSc1>{rj, rs});
         if (job) {
             rj.finish(rs);
             if (rj.n > blockDim.x)
                 cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, it.idx, a.region, a.cr,
                                             (int)(threadIdx.x + blockDim.x), (int)blockDim.x);
         }
-        flow_signal(flow_ctr(a.ctl, q, slot, 1));
+        return flow_ctr(a.ctl, q, slot, 1);
     } else if (it.kind == 2) {   // the last CPI's range stage: one hit region
         if (threadIdx.x == 0) flow_wait(flow_ctr(a.ctl, q, slot, 1), (gen + 1) * (uint32_t)a.nm, st);
         __syncthreads();
+        stamp(2);
         const RangeSrc rs = src_of(j);
         cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, it.idx, a.region, a.cr, (int)threadIdx.x,
                                     (int)blockDim.x);
     }
+    return nullptr;
 }
 
+// minimum waves per SIMD of the dataflow kernel (4 = four workgroups per CU, <= 128 VGPRs: the
+// residency of the chunked kernels; dev-only -D for A/B)
+#ifndef RSP_FLOW_WAVES
+#define RSP_FLOW_WAVES 4
+#endif
 template <typename TIn, int N1, int N2, int P, int REF>
-__global__ __launch_bounds__(kBlock, 4) void flow_kernel(FlowArgs a) {
+__global__ __launch_bounds__(kBlock, RSP_FLOW_WAVES) void flow_kernel(FlowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint32_t s_item, s_hits;
     const int nh = (a.flag && a.cr.rflag && a.m.cv.enabled) ? a.nm : 0;
@@ -1834,21 +1889,27 @@ __global__ __launch_bounds__(kBlock, 4) void flow_kernel(FlowArgs a) {
     __syncthreads();
     uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
     int tried = 1;
+#ifdef RSP_DIAG_FLOW
+    int ndiag = 0;
+#endif
+    // Per item: decode, thread 0 waits for the item's inputs, barrier, body, thread 0 claims the
+    // next item, every wave drains its stores, barrier, thread 0 publishes the item and the next
+    // item number, barrier.  (Each thread-0 region is fenced by barriers: a block holding a barrier is
+    // never duplicated, so jump threading cannot join two thread-0 regions across the back edge --
+    // which splits the loop into nested loops with a divergent exit, and lanes 1-63 of wave 0
+    // then run the body's barriers without thread 0: tools/micro/handoff_probe.hip.)
     for (;;) {
-        __syncthreads();   // every thread has read s_item
         if (k >= flow_total(a, h, nh)) {   // this queue is drained: help the next one
             if (tried == kFlowQueues) break;
             ++tried;
             h = (h + 1) % kFlowQueues;
+            __syncthreads();   // every thread has read s_item
             if (threadIdx.x == 0)
                 s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
             k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
             continue;
         }
-        uint32_t nxt = 0;
-        if (threadIdx.x == 0)   // claim ahead: the atomic's latency hides under the item
-            nxt = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // The item reads its arguments through an opaque copy of the kernarg pointer: otherwise
         // hipcc hoists every field any item type uses into SGPRs for the whole loop (hundreds of
         // SGPR spills into VGPR lanes, then VGPR spills).  The pointer stays constant-address-space,
@@ -1858,9 +1919,34 @@ __global__ __launch_bounds__(kBlock, 4) void flow_kernel(FlowArgs a) {
         asm volatile("" : "+s"(ap));
         const FlowArgs& ai = *(const FlowArgs*)ap;
         const FlowItem it = flow_decode(ai, h, nh, k);
-        flow_item<TIn, N1, N2, P, REF>(ai, h, it, nh, smem, &s_hits);
+        uint64_t* diag = nullptr;
+#ifdef RSP_DIAG_FLOW
+        if (blockIdx.x < (unsigned)kFlowDiagWG && ndiag < kFlowDiagItems) {
+            diag = g_flow_diag + ((size_t)blockIdx.x * kFlowDiagItems + ndiag) * 4;
+            if (threadIdx.x == 0) {
+                diag[0] = (uint64_t)(it.kind + 1) | ((uint64_t)(uint32_t)it.j << 4) | ((uint64_t)(uint32_t)it.idx << 36);
+                diag[1] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
+        ++ndiag;
+#endif
+        uint32_t* sig = flow_item<TIn, N1, N2, P, REF>(ai, h, it, nh, smem, &s_hits, diag);
+        // claim the next item behind the item's last stores: the atomic's round trip overlaps the
+        // drain below (claimed earlier, its return would hold up the first vmcnt wait of the item)
+        uint32_t nxt = 0;
+        if (threadIdx.x == 0)
+            nxt = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef RSP_FLOW_NODRAIN   // (dev-only timing switch: publishing before the stores land is wrong)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done (sc1: in memory)
+#endif
         __syncthreads();
-        if (threadIdx.x == 0) s_item = nxt;
+        if (threadIdx.x == 0) {
+            if (sig) __hip_atomic_fetch_add((gu32*)sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_item = nxt;
+        }
+#ifdef RSP_DIAG_FLOW
+        if (diag && threadIdx.x == 0) diag[3] = __builtin_amdgcn_s_memrealtime();
+#endif
         __syncthreads();
         k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
     }
@@ -1898,6 +1984,25 @@ static hipError_t launch_flow_t(FlowArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((flow_kernel<TIn, N1, N2, P, REF>), dim3((unsigned)grid), dim3(kBlock), lds, s, a);
     return hipGetLastError();
 }
+
+#ifdef RSP_DIAG_FLOW
+}  // namespace rsp
+// Dev-only diagnostic export (not in include/rsp.h): the dataflow kernel's item stamps.
+extern "C" int rsp_diag_flow(uint64_t* host, int64_t n) {
+    if (n < 0 || n > (int64_t)rsp::kFlowDiagWG * rsp::kFlowDiagItems * 4) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsp::g_flow_diag), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0 : -3;
+}
+extern "C" int rsp_diag_flow_clear() {
+    static uint64_t zero[4096] = {};
+    for (size_t o = 0; o < sizeof(rsp::g_flow_diag); o += sizeof(zero))
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rsp::g_flow_diag), zero, sizeof(zero), o, hipMemcpyHostToDevice) != hipSuccess)
+            return -1;
+    return 0;
+}
+namespace rsp {
+#endif
 
 bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams) {
     return beams == 1 && P == 128 && nfft1 == 1024 && nfft2 == 4096 && (dtype == RSP_C64 || dtype == RSP_C32F16);

@@ -60,27 +60,20 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         }
         mexAtExit(cleanup);
     }
-    const size_t n = (size_t)(V * R);
-    const double* in = mxGetDoubles(M);
-    float* r32 = (float*)mxMalloc(n * sizeof(float));
-    uint8_t* f = (uint8_t*)mxMalloc(n);
-    uint8_t* fv = (uint8_t*)mxMalloc(n);
-    for (size_t i = 0; i < n; ++i) r32[i] = (float)in[i];
-    int rc = rsp_cfar(g_ctx, r32, RSP_COLMAJOR, V, R, 1, &cf, f, fv);
+    /* double in, double 0/1 out: the narrowing and widening run on the library's copy threads,
+     * piece by piece beside the DMA (rsp_cfar_f64) */
+    plhs[0] = mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL);
+    mxArray* fv = nlhs > 1 ? mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL) : NULL;
+    int rc = rsp_cfar_f64(g_ctx, mxGetDoubles(M), RSP_COLMAJOR, V, R, 1, &cf, mxGetDoubles(plhs[0]),
+                          fv ? mxGetDoubles(fv) : NULL);
     if (rc != RSP_OK) {
         char msg[512];
         strncpy(msg, rsp_last_error(g_ctx), sizeof(msg) - 1);
         msg[sizeof(msg) - 1] = 0;
-        mxFree(r32); mxFree(f); mxFree(fv);
+        mxDestroyArray(plhs[0]);
+        plhs[0] = NULL;
+        if (fv) mxDestroyArray(fv);
         mexErrMsgIdAndTxt(rc == RSP_ERR_CFAR_WINDOW ? "rsp:cfar_window" : "rsp:run", "%s", msg);
     }
-    plhs[0] = mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL);
-    double* o = mxGetDoubles(plhs[0]);
-    for (size_t i = 0; i < n; ++i) o[i] = f[i];
-    if (nlhs > 1) {
-        plhs[1] = mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL);
-        double* ov = mxGetDoubles(plhs[1]);
-        for (size_t i = 0; i < n; ++i) ov[i] = fv[i];
-    }
-    mxFree(r32); mxFree(f); mxFree(fv);
+    if (fv) plhs[1] = fv;
 }

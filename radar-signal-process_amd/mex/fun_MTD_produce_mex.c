@@ -157,17 +157,17 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         memcpy(g_key, key, sizeof(key));
         mexAtExit(cleanup);
     }
-    float* rdm = (float*)mxMalloc((size_t)(P * R) * sizeof(float));
-    int rc = rsp_pc_mtd(g_ctx, mxGetComplexDoubles(E), RSP_C128, RSP_COLMAJOR, P, R, 1, rdm, RSP_COLMAJOR);
+    /* the RDM lands in MATLAB's double matrix directly: the library widens each device->host
+     * piece on its copy threads as the piece arrives (rsp_pc_mtd_cfar_f64, cfar = NULL) */
+    plhs[0] = mxCreateDoubleMatrix((mwSize)P, (mwSize)R, mxREAL);
+    int rc = rsp_pc_mtd_cfar_f64(g_ctx, mxGetComplexDoubles(E), RSP_C128, RSP_COLMAJOR, P, R, 1, NULL,
+                                 mxGetDoubles(plhs[0]), RSP_COLMAJOR, NULL, NULL);
     if (rc != RSP_OK) {
         char msg[512];
         strncpy(msg, rsp_last_error(g_ctx), sizeof(msg) - 1);
         msg[sizeof(msg) - 1] = 0;
-        mxFree(rdm);
+        mxDestroyArray(plhs[0]);
+        plhs[0] = NULL;
         mexErrMsgIdAndTxt("rsp:run", "%s", msg);
     }
-    plhs[0] = mxCreateDoubleMatrix((mwSize)P, (mwSize)R, mxREAL);
-    double* out = mxGetDoubles(plhs[0]);
-    for (int64_t i = 0; i < P * R; ++i) out[i] = rdm[i];
-    mxFree(rdm);
 }

@@ -31,7 +31,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_set_host_pipeline", "rsp_ingest_record_bytes",
            "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter",
-           "rsp_set_flow", "rsp_flow_status")
+           "rsp_set_flow", "rsp_flow_status", "rsp_pc_mtd_cfar_f64", "rsp_cfar_f64")
 RSP_NKERNELS = 5
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "flow_kernel")
 
@@ -120,6 +120,11 @@ def load_library(path=None):
     lib.rsp_pc_mtd_cfar.restype = C.c_int
     lib.rsp_pc_mtd_cfar.argtypes = [vp, vp, i32, i32, i64, i64, i64, C.POINTER(rsp_cfar_params),
                                     vp, i32, vp, vp]
+    lib.rsp_pc_mtd_cfar_f64.restype = C.c_int
+    lib.rsp_pc_mtd_cfar_f64.argtypes = [vp, vp, i32, i32, i64, i64, i64, C.POINTER(rsp_cfar_params),
+                                        vp, i32, vp, vp]
+    lib.rsp_cfar_f64.restype = C.c_int
+    lib.rsp_cfar_f64.argtypes = [vp, vp, i32, i64, i64, i64, C.POINTER(rsp_cfar_params), vp, vp]
     lib.rsp_pc_mtd_cfar_dev.restype = C.c_int
     lib.rsp_pc_mtd_cfar_dev.argtypes = [vp, vp, i32, i64, C.POINTER(rsp_cfar_params), vp, vp, vp, vp]
     lib.rsp_cfar_dev.restype = C.c_int

@@ -22,6 +22,7 @@ mxComplexDouble* mxGetComplexDoubles(const mxArray*);
 mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
 void* mxMalloc(size_t);
 void mxFree(void*);
+void mxDestroyArray(mxArray*);
 void mexErrMsgIdAndTxt(const char*, const char*, ...);
 int mexAtExit(void (*)(void));
 #endif

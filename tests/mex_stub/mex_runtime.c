@@ -102,6 +102,7 @@ void rt_free(mxArray* a) {
     free(a->re);
     free(a);
 }
+void mxDestroyArray(mxArray* a) { rt_free(a); }
 size_t rt_m(const mxArray* a) { return a->m; }
 size_t rt_n(const mxArray* a) { return a->n; }
 int rt_is_complex(const mxArray* a) { return a->is_complex; }

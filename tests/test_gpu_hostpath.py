@@ -121,3 +121,48 @@ def test_host_path_two_beam_dmx(torch_cuda, chunk):
     rdm2, flag2, _ = eng.pc_mtd_cfar(e, cf, want_flagV=False)   # row-major complex64
     assert np.array_equal(rdm2, want[0]) and np.array_equal(flag2, want[1])
     eng.close()
+
+
+def test_f64_entry_points_equal_float_forms(torch_cuda):
+    """rsp_pc_mtd_cfar_f64 / rsp_cfar_f64 (MATLAB's double outputs and input, widened / narrowed
+    on the copy threads piece by piece): the same values as the float / byte forms, exactly, for
+    one CPI per call (the MEX granularity) and a chunked batch, in both layouts."""
+    import ctypes as C
+    from rsp import _capi as capi
+    from rsp import presets, synth
+    eng = _engine(128, 4096)
+    cf = presets.default_cfar(eng.spec)
+    cp = cf.to_c()
+    lib = eng.lib
+    V, Ro = eng.shape
+    P, R = eng.spec.P, eng.spec.R
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None   # noqa: E731
+    for B, chunk, lay in ((1, 0, capi.RSP_COLMAJOR), (5, 2, capi.RSP_ROWMAJOR)):
+        eng.set_host_pipeline(chunk, 0)
+        echo = synth.echo_numpy(eng.spec, B, seed=900 + B).astype(np.complex128)
+        if lay == capi.RSP_COLMAJOR:
+            echo = np.ascontiguousarray(np.swapaxes(echo, 1, 2))
+        oshape = (B, V, Ro) if lay == capi.RSP_ROWMAJOR else (B, Ro, V)
+        r32, f8, v8 = np.empty(oshape, np.float32), np.empty(oshape, np.uint8), np.empty(oshape, np.uint8)
+        assert lib.rsp_pc_mtd_cfar(eng.ctx, ptr(echo), capi.RSP_C128, lay, P, R, B, C.byref(cp), ptr(r32), lay,
+                                   ptr(f8), ptr(v8)) == 0
+        r64, f64, v64 = (np.full(oshape, np.nan), np.full(oshape, 7.0), np.full(oshape, 7.0))
+        assert lib.rsp_pc_mtd_cfar_f64(eng.ctx, ptr(echo), capi.RSP_C128, lay, P, R, B, C.byref(cp), ptr(r64), lay,
+                                       ptr(f64), ptr(v64)) == 0
+        assert np.array_equal(r64, r32.astype(np.float64))
+        assert np.array_equal(f64, f8.astype(np.float64)) and np.array_equal(v64, v8.astype(np.float64))
+        # RDM only (fun_MTD_produce)
+        r64b = np.full(oshape, np.nan)
+        assert lib.rsp_pc_mtd_cfar_f64(eng.ctx, ptr(echo), capi.RSP_C128, lay, P, R, B, None, ptr(r64b), lay,
+                                       None, None) == 0
+        assert np.array_equal(r64b, r64)
+        # executeCFAR on that RDM, double in / out, against the float form
+        rin = r64.astype(np.float64)
+        cf8, cv8 = np.empty(oshape, np.uint8), np.empty(oshape, np.uint8)
+        assert lib.rsp_cfar(eng.ctx, ptr(np.ascontiguousarray(rin.astype(np.float32))), lay, V, Ro, B, C.byref(cp),
+                            ptr(cf8), ptr(cv8)) == 0
+        cf64, cv64 = np.full(oshape, 7.0), np.full(oshape, 7.0)
+        assert lib.rsp_cfar_f64(eng.ctx, ptr(rin), lay, V, Ro, B, C.byref(cp), ptr(cf64), ptr(cv64)) == 0
+        assert np.array_equal(cf64, cf8.astype(np.float64)) and np.array_equal(cv64, cv8.astype(np.float64))
+        assert cf64.sum() > 0
+    eng.close()

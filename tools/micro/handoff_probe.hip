@@ -170,6 +170,17 @@ __global__ __launch_bounds__(kT) void flow(Args a) {
     }
 }
 
+// which XCC each workgroup of a grid runs on (HW_REG_XCC_ID, raw bits), and whether it equals
+// blockIdx.x % 8 shifted by the XCC of block 0
+__global__ __launch_bounds__(kT) void xcc_census(uint32_t* hist, uint32_t* raw) {
+    if (threadIdx.x == 0) {
+        uint32_t v;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 16)" : "=s"(v));
+        raw[blockIdx.x] = v;
+        atomicAdd(hist + (v & 15u), 1u);
+    }
+}
+
 __global__ __launch_bounds__(kT) void prod_launch(Args a, int r) {
     const int q = blockIdx.x / a.G, item = blockIdx.x % a.G;
     produce<3>(a, q, r, item);
@@ -196,6 +207,24 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
+    {
+        uint32_t *hist, *raw;
+        hipMalloc(&hist, 16 * 4);
+        hipMalloc(&raw, grid * 4);
+        hipMemset(hist, 0, 64);
+        hipLaunchKernelGGL(xcc_census, dim3(grid), dim3(kT), 0, 0, hist, raw);
+        std::vector<uint32_t> h(16), r(grid);
+        hipMemcpy(h.data(), hist, 64, hipMemcpyDeviceToHost);
+        hipMemcpy(r.data(), raw, grid * 4, hipMemcpyDeviceToHost);
+        int match = 0;
+        for (int b = 0; b < grid; ++b) match += (r[b] & 15u) == ((r[0] + b) & 7u);
+        printf("XCC_ID census over %d workgroups:", grid);
+        for (int i = 0; i < 16; ++i)
+            if (h[i]) printf(" [%d]=%u", i, h[i]);
+        printf("; raw[0..9] = %x %x %x %x %x %x %x %x %x %x; blockIdx %% 8 + XCC(0) matches %d\n", r[0], r[1], r[2], r[3],
+               r[4], r[5], r[6], r[7], r[8], r[9], match);
+        fflush(stdout);
+    }
     printf("grid %d workgroups (%d CUs); %d rounds per queue, 8 queues; 32 KB items\n", grid, cus, rounds);
     for (int G : Gs) {
         a.G = G;
