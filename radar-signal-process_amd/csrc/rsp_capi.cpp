@@ -8,6 +8,7 @@
 // the fast-time (PC) and slow-time (MTD) passes is served on-die instead of from HBM.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <cstdarg>
@@ -498,6 +499,7 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
             if (pc.seg[s].kind != RSP_SEG_MF) continue;
             rsp::PcMfArgs a;
             std::memset(&a, 0, sizeof(a));
+            a.cpi_rows = (int)p.P;
             a.R = (int)p.R;
             a.R_out = (int)p.R_out;
             a.mf = pc.seg[s];
@@ -1657,9 +1659,31 @@ int rsp_pc_mtd_cfar_f64(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t l
     return host_call(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out, true);
 }
 
+// Dev-only host-path trace (environment RSP_HOST_TRACE=1): per call, host time of the setup, the
+// input staging (narrowing + DMA issue), the chain enqueue, the output staging (waits + widening)
+// and the final syncs, plus device time of the H2D / chain / D2H streams (timing events), on
+// stderr.  Used by tools/mex_bench.py --trace to find where a one-CPI MEX call spends its time.
+struct HostTrace {
+    bool on = false;
+    std::chrono::steady_clock::time_point t[8];
+    int n = 0;
+    hipEvent_t e[6] = {};
+    void mark() { if (on && n < 8) t[n++] = std::chrono::steady_clock::now(); }
+    void ev(int i, hipStream_t st) { if (on) (void)hipEventRecord(e[i], st); }
+};
+static bool host_trace_on() {
+    static const bool on = [] { const char* v = getenv("RSP_HOST_TRACE"); return v && *v == '1'; }();
+    return on;
+}
+
 static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
                       int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout,
                       void* flag_out, void* flagV_out, bool f64) {
+    HostTrace ht;
+    ht.on = host_trace_on();
+    if (ht.on)
+        for (auto& e : ht.e) (void)hipEventCreate(&e);
+    ht.mark();
     int rc = check_host_call(ctx, echo, dtype, layout, P, R, batch);
     if (rc) return rc;
     if (out_layout != RSP_ROWMAJOR && out_layout != RSP_COLMAJOR) return fail(ctx, RSP_ERR_ARG, "bad out_layout");
@@ -1744,20 +1768,48 @@ static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t lay
         HIP_TRY(ctx, hipEventRecord(h.ev_out[sl], h.s_d2h));
         return RSP_OK;
     };
+    ht.mark();   // 1: set up
     for (int64_t k = 0; k < nk; ++k) {
         const int sl = (int)(k % h.kSlots);
         // the slot's previous chain (chunk k-2) has read its input
         if (k >= h.kSlots) HIP_TRY(ctx, hipStreamWaitEvent(h.s_h2d, h.ev_comp[sl], 0));
+        if (k == 0) ht.ev(0, h.s_h2d);
         if ((rc = h2d_pieces(ctx, h.in[sl].p, (const char*)echo + (size_t)k * K * in_cpi, (size_t)chunk_n(k) * dev_cpi,
                              narrow ? 1 : 0)))
             return rc;
+        if (k == nk - 1) ht.ev(1, h.s_h2d);
         HIP_TRY(ctx, hipEventRecord(h.ev_in[sl], h.s_h2d));
+        if (k == 0) ht.mark();   // 2: first chunk staged
+        if (k == 0) {
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_in[sl], 0));
+            ht.ev(2, ctx->stream);
+        }
         if ((rc = compute(k))) return rc;
+        if (k == nk - 1) ht.ev(3, ctx->stream);
+        if (k == 0) ht.mark();   // 3: first chain enqueued
         if (k >= 1 && (rc = output(k - 1))) return rc;
     }
+    if (ht.on) {
+        HIP_TRY(ctx, hipStreamWaitEvent(h.s_d2h, h.ev_comp[(nk - 1) % h.kSlots], 0));
+        ht.ev(4, h.s_d2h);
+    }
     if ((rc = output(nk - 1))) return rc;
+    ht.ev(5, h.s_d2h);
+    ht.mark();   // 4: outputs staged
     HIP_TRY(ctx, hipStreamSynchronize(h.s_d2h));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ht.mark();   // 5: done
+    if (ht.on) {
+        float g[3] = {};
+        (void)hipEventElapsedTime(&g[0], ht.e[0], ht.e[1]);
+        (void)hipEventElapsedTime(&g[1], ht.e[2], ht.e[3]);
+        (void)hipEventElapsedTime(&g[2], ht.e[4], ht.e[5]);
+        auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(ht.t[b] - ht.t[a]).count(); };
+        fprintf(stderr, "rsp_host_trace batch %lld chunks %lld host_us setup %.1f stage_in %.1f enqueue %.1f stage_out %.1f "
+                "sync %.1f total %.1f dev_us h2d %.1f chain %.1f d2h %.1f\n", (long long)batch, (long long)nk, us(0, 1),
+                us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(0, 5), g[0] * 1e3, g[1] * 1e3, g[2] * 1e3);
+        for (auto& e : ht.e) (void)hipEventDestroy(e);
+    }
     return RSP_OK;
 }
 

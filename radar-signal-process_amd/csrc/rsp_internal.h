@@ -74,6 +74,7 @@ struct PcMfArgs {
     // output wraps.  nsub <= 1: the whole segment in one mf.nfft-point transform.
     int nsub, sub_step;
     const float* gain;   // fused iSTC (rsp_set_prefilter): echo column n scaled by gain[n], or null
+    int cpi_rows;        // PRT rows per CPI (dev-only -DRSP_XCD_AFFINITY block mapping)
     int nzero;
     int zero_lo[RSP_MAX_SEG + 1];
     int zero_hi[RSP_MAX_SEG + 1];

@@ -471,6 +471,24 @@ __device__ __forceinline__ void pc_mf_block(const TIn* __restrict__ echo, float2
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
     // unit u of a segment = (row u / nsub, overlap-save sub-block u % nsub)
+#ifdef RSP_XCD_AFFINITY
+    // (dev-only A/B of VERDICT r4 item 1b) the rows of CPI c go to blocks b with b % 8 == c % 8,
+    // i.e. to one XCD under round-robin dealing, where the MTD tiles of CPI c (same mapping in
+    // mtd_block) read them: chunks of a multiple of 8 CPIs, one segment-2 row per block
+    if constexpr (N2 != 0 && PC::RPB2 == 1) {
+        const int P = a2.cpi_rows, ncpi = a2.rows / (P > 0 ? P : 1);
+        if (P > 0 && ncpi % 8 == 0 && P % PC::RPB1 == 0 && a2.nsub <= 1 && a1.nsub <= 1) {
+            const int x = bid % 8, sl = bid / 8;
+            if (bid < nblk2) {
+                bid = (x + 8 * (sl / P)) * P + sl % P;
+            } else {
+                const int b = bid - nblk2, gpc = P / PC::RPB1;   // short-row groups per CPI
+                const int s2 = b / 8;
+                bid = nblk2 + (x + 8 * (s2 / gpc)) * gpc + s2 % gpc;
+            }
+        }
+    }
+#endif
     if constexpr (N2 != 0) {
         if (bid < nblk2) {
             constexpr int G = PcCfg<N2>::G;
@@ -1361,6 +1379,14 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
                                           uint8_t* __restrict__ flagV, const MtdArgs& a, int bx, int by, int gx, int gy,
                                           unsigned char* smem, uint32_t* s_hits) {
     using C = MtdCfg<P, BEAMS>;
+#ifdef RSP_XCD_AFFINITY
+    // (dev-only, see pc_mf_block) the tiles of CPI c on blocks with linear id % 8 == c % 8
+    if (a.nwin == 0 && gy % 8 == 0 && gx % 8 == 0) {
+        const int lin = by * gx + bx, x = lin % 8, sl = lin / 8;
+        by = x + 8 * (sl / gx);
+        bx = sl % gx;
+    }
+#endif
     const size_t cpi = (size_t)by;
     const size_t R = (size_t)a.R_out;
     const size_t plane = (size_t)P * R;

@@ -154,7 +154,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--compare", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--trace", action="store_true",
+                    help="RSP_HOST_TRACE=1: the library prints a per-call phase breakdown on stderr")
     a = ap.parse_args()
+    if a.trace:
+        os.environ["RSP_HOST_TRACE"] = "1"
     out = run(a.P, a.R, a.seconds, a.compare)
     print(json.dumps(out))
     if a.json:
