@@ -61,9 +61,16 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         mexAtExit(cleanup);
     }
     /* double in, double 0/1 out: the narrowing and widening run on the library's copy threads,
-     * piece by piece beside the DMA (rsp_cfar_f64) */
-    plhs[0] = mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL);
-    mxArray* fv = nlhs > 1 ? mxCreateDoubleMatrix((mwSize)V, (mwSize)R, mxREAL) : NULL;
+     * piece by piece beside the DMA (rsp_cfar_f64).  Every flag element is written, so the
+     * outputs skip MATLAB's zero fill (mxCreateUninitNumericMatrix, R2015a+) */
+    plhs[0] = mxCreateUninitNumericMatrix((size_t)V, (size_t)R, mxDOUBLE_CLASS, mxREAL);
+    mxArray* fv = nlhs > 1 ? mxCreateUninitNumericMatrix((size_t)V, (size_t)R, mxDOUBLE_CLASS, mxREAL) : NULL;
+    if (!plhs[0] || (nlhs > 1 && !fv)) {
+        if (plhs[0]) mxDestroyArray(plhs[0]);
+        plhs[0] = NULL;
+        if (fv) mxDestroyArray(fv);
+        mexErrMsgIdAndTxt("rsp:nomem", "cannot allocate the %lld x %lld flag planes", (long long)V, (long long)R);
+    }
     int rc = rsp_cfar_f64(g_ctx, mxGetDoubles(M), RSP_COLMAJOR, V, R, 1, &cf, mxGetDoubles(plhs[0]),
                           fv ? mxGetDoubles(fv) : NULL);
     if (rc != RSP_OK) {

@@ -9,6 +9,7 @@ typedef struct mxArray_tag mxArray;
 typedef size_t mwSize;
 typedef struct { double real, imag; } mxComplexDouble;
 typedef enum { mxREAL = 0, mxCOMPLEX = 1 } mxComplexity;
+typedef enum { mxUNKNOWN_CLASS = 0, mxDOUBLE_CLASS = 6 } mxClassID;
 int mxIsDouble(const mxArray*);
 int mxIsComplex(const mxArray*);
 int mxIsStruct(const mxArray*);
@@ -20,6 +21,7 @@ double mxGetScalar(const mxArray*);
 double* mxGetDoubles(const mxArray*);
 mxComplexDouble* mxGetComplexDoubles(const mxArray*);
 mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
+mxArray* mxCreateUninitNumericMatrix(size_t, size_t, mxClassID, mxComplexity);
 void* mxMalloc(size_t);
 void mxFree(void*);
 void mxDestroyArray(mxArray*);

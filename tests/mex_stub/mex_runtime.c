@@ -53,6 +53,17 @@ mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity c) {
     a->re = (double*)calloc(m * n * (a->is_complex ? 2 : 1) + 1, sizeof(double));
     return a;
 }
+/* MATLAB's uninitialised allocation (R2015a+): the same array without the zero fill -- in
+ * this fake, malloc instead of calloc (only mxDOUBLE_CLASS, the one class the shims create) */
+mxArray* mxCreateUninitNumericMatrix(size_t m, size_t n, mxClassID cls, mxComplexity c) {
+    if (cls != mxDOUBLE_CLASS) return NULL;
+    mxArray* a = (mxArray*)calloc(1, sizeof(mxArray));
+    a->m = m;
+    a->n = n;
+    a->is_complex = c == mxCOMPLEX;
+    a->re = (double*)malloc((m * n * (a->is_complex ? 2 : 1) + 1) * sizeof(double));
+    return a;
+}
 void* mxMalloc(size_t n) { return malloc(n); }
 void mxFree(void* p) { free(p); }
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) {
