@@ -8,6 +8,7 @@
 // the fast-time (PC) and slow-time (MTD) passes is served on-die instead of from HBM.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <complex>
@@ -93,6 +94,12 @@ struct rsp_ctx {
         int ring_in = 0;                      // next input piece slot
         int threads = 0;                      // requested copy threads (0 = default)
         std::unique_ptr<rsp::CopyPool> pool;
+        // one-chunk calls (host_chain_small): pinned staging the kernels read and write directly
+        static constexpr int kParts = 16;     // output parts in flight (one event each)
+        void* zc_in = nullptr;
+        void* zc_out = nullptr;
+        size_t zc_in_n = 0, zc_out_n = 0;
+        hipEvent_t ev_part[kParts] = {};
     } hp;
     int64_t host_chunk = 0;                   // CPIs per host chunk (0 = by bytes)
     // diagnostics (rsp_profile): HIP event pairs around each kernel launch
@@ -322,6 +329,10 @@ int rsp_destroy(rsp_ctx* ctx) {
             if (h.ev_comp[i]) hipEventDestroy(h.ev_comp[i]);
             if (h.ev_out[i]) hipEventDestroy(h.ev_out[i]);
         }
+        if (h.zc_in) hipHostFree(h.zc_in);
+        if (h.zc_out) hipHostFree(h.zc_out);
+        for (auto& e : h.ev_part)
+            if (e) hipEventDestroy(e);
         for (int i = 0; i < h.kRing; ++i) {
             if (h.pin_in[i]) hipHostFree(h.pin_in[i]);
             if (h.pin_out[i]) hipHostFree(h.pin_out[i]);
@@ -1497,6 +1508,7 @@ static int host_pipe_init(rsp_ctx* ctx) {
         HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_comp[i], hipEventDisableTiming));
         HIP_TRY(ctx, hipEventCreateWithFlags(&h.ev_out[i], hipEventDisableTiming));
     }
+    for (auto& e : h.ev_part) HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h.piece = kHostPiece;
     for (int i = 0; i < h.kRing; ++i) {
         HIP_TRY(ctx, hipHostMalloc(&h.pin_in[i], h.piece, hipHostMallocDefault));
@@ -1668,12 +1680,217 @@ struct HostTrace {
     std::chrono::steady_clock::time_point t[8];
     int n = 0;
     hipEvent_t e[6] = {};
+    double acc[4] = {};   // one-chunk path: input conversion, output waits, output conversion (us)
     void mark() { if (on && n < 8) t[n++] = std::chrono::steady_clock::now(); }
+    double now_us() const {
+        return on ? std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count() : 0.0;
+    }
     void ev(int i, hipStream_t st) { if (on) (void)hipEventRecord(e[i], st); }
 };
 static bool host_trace_on() {
     static const bool on = [] { const char* v = getenv("RSP_HOST_TRACE"); return v && *v == '1'; }();
     return on;
+}
+
+// One-chunk calls (MATLAB's granularity: fun_MTD_produce is one CPI per call) are latency-bound,
+// not bandwidth-bound: a pinned DMA pays ~13 us of fixed cost per copy and ~11 us more to
+// signal the host (tools/micro/host_latency_probe.hip, profiles/r05/mex/), and the host's
+// narrowing / widening sat between DMAs on the critical path.  Here the kernels move the data
+// across PCIe themselves:
+//   * input: the copy threads narrow (or copy) the caller's echo into pinned staging in pieces
+//     of ~1 MiB that never cross a plane; right behind each piece, a transpose (column-major) or
+//     copy (row-major) kernel on the chain's stream reads it from pinned memory into the
+//     chain's device input -- PCIe transfer, ingest transpose and host narrowing overlap;
+//   * output: after the chain, transpose / copy kernels write the RDM and flag planes into
+//     pinned staging in up to kParts parts, an event behind each; the copy threads widen (or
+//     copy) part q into the caller's arrays while parts q+1.. cross the link.
+// Staging is allocated coherent (fine-grained: not cached in the GPU's L2), so a kernel never
+// reads a previous call's input from L2 and the host never reads output lines the L2 still holds.
+// RSP_HOST_ZC=0 (dev A/B) restores the DMA pipeline for every call.
+static constexpr size_t kZcPiece = 1u << 20;       // device bytes per input piece
+static constexpr size_t kZcMaxIn = 64u << 20;      // one-chunk calls up to this much device input
+static int zc_knob(const char* name, int dflt) {   // dev A/B knobs of the one-chunk path
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+static int zc_mode() {
+    static const int m = [] { const char* v = getenv("RSP_HOST_ZC"); return v && *v ? atoi(v) : 1; }();
+    return m;
+}
+static int zc_ensure(rsp_ctx* ctx, void** p, size_t* n, size_t bytes) {
+    if (*p && *n >= bytes) return RSP_OK;
+    if (*p) {
+        HIP_TRY(ctx, hipHostFree(*p));
+        *p = nullptr;
+        *n = 0;
+    }
+    HIP_TRY(ctx, hipHostMalloc(p, bytes, zc_mode() == 2 ? hipHostMallocDefault : hipHostMallocCoherent));
+    *n = bytes;
+    return RSP_OK;
+}
+
+// Output delivery of the one-chunk paths: planes [batch][V][Ro] of each output (device, `es`
+// bytes per element: 4 float, 1 byte) are transposed (tr: the caller's column-major [Ro][V]) or
+// copied into pinned staging by kernels on ctx->stream, in parts of whole range-bin rows with an
+// event behind each; the copy threads deliver part q -- widened to double when f64 -- into the
+// caller's array while the later parts cross the link.
+struct ZcOut {
+    const void* dev;
+    int es;
+    void* host;
+    bool f64;
+};
+static int zc_deliver(rsp_ctx* ctx, const ZcOut* outs, int nout, int64_t batch, int64_t V, int64_t Ro, bool tr,
+                      HostTrace& ht) {
+    auto& h = ctx->hp;
+    const size_t cells = (size_t)V * Ro, ocells = (size_t)batch * cells;
+    size_t bytes = 0;
+    for (int k = 0; k < nout; ++k) bytes += ocells * outs[k].es;
+    int rc;
+    if ((rc = zc_ensure(ctx, &h.zc_out, &h.zc_out_n, bytes))) return rc;
+    hipStream_t st = ctx->stream;
+    struct Part {
+        int k;
+        size_t off, n;
+    };
+    Part parts[rsp_ctx::HostPipe::kParts];
+    int np = 0;
+    // parts of >= ~1 MiB of device output (a part costs a kernel and an event: at c3, 2 parts of
+    // the 2 MiB RDM beat 4 of 512 KiB; executeCFAR's ~170 KB segments go whole), within kParts
+    static const size_t kPartBytes = (size_t)zc_knob("RSP_ZC_PART_KIB", 1024) << 10;
+    const int budget = h.kParts / (nout * (int)batch);
+    char* zk[3] = {};
+    size_t zoff = 0;
+    for (int k = 0; k < nout; ++k) {
+        zk[k] = (char*)h.zc_out + zoff;
+        zoff += ocells * outs[k].es;
+    }
+    for (int k = 0; k < nout; ++k) {
+        const size_t es = (size_t)outs[k].es;
+        const int elem = es == 4 ? rsp::RSP_SUB_F32 : rsp::RSP_SUB_U8;
+        int per_plane = (int)((cells * es + kPartBytes / 2) / kPartBytes);
+        per_plane = per_plane < 1 ? 1 : (per_plane > budget ? budget : per_plane);
+        if (tr) {   // plane b: [V][Ro] -> [Ro][V]; a part = output rows [c0, c1) (range bins)
+            int64_t cp = (Ro + per_plane - 1) / per_plane;
+            cp = (cp + 31) / 32 * 32;
+            for (int64_t b = 0; b < batch; ++b)
+                for (int64_t c0 = 0; c0 < Ro; c0 += cp) {
+                    const int64_t c1 = c0 + cp < Ro ? c0 + cp : Ro;
+                    HIP_TRY(ctx, rsp::launch_transpose_sub(elem, (const char*)outs[k].dev + ((size_t)b * cells + c0) * es,
+                                                           zk[k] + (size_t)(b * Ro + c0) * V * es, (int)V, (int)(c1 - c0),
+                                                           (size_t)Ro, (size_t)V, st));
+                    HIP_TRY(ctx, hipEventRecord(h.ev_part[np], st));
+                    parts[np++] = {k, (size_t)(b * Ro + c0) * V, (size_t)(c1 - c0) * V};
+                }
+        } else {    // row-major: contiguous parts (whole 4-byte words: ocells % 4 == 0, checked)
+            const int nparts = per_plane * (int)batch;
+            size_t pe = (ocells + nparts - 1) / nparts;
+            pe = (pe + 1023) / 1024 * 1024;
+            for (size_t off = 0; off < ocells; off += pe) {
+                const size_t n = ocells - off < pe ? ocells - off : pe;
+                HIP_TRY(ctx, rsp::launch_copy_words((const char*)outs[k].dev + off * es, zk[k] + off * es, n * es / 4, st));
+                HIP_TRY(ctx, hipEventRecord(h.ev_part[np], st));
+                parts[np++] = {k, off, n};
+            }
+        }
+    }
+    ht.mark();   // 3: chain and output kernels enqueued
+    rsp::CopyPool& pool = host_pool(ctx);
+    for (int q = 0; q < np; ++q) {
+        const Part& pt = parts[q];
+        const ZcOut& o = outs[pt.k];
+        const double t0 = ht.now_us();
+        HIP_TRY(ctx, hipEventSynchronize(h.ev_part[q]));
+        const double t1 = ht.now_us();
+        const char* zp = zk[pt.k] + pt.off * o.es;
+        if (o.es == 4) {
+            if (o.f64) pool.widen_f32((double*)o.host + pt.off, (const float*)zp, pt.n);
+            else pool.copy((float*)o.host + pt.off, zp, pt.n * 4);
+        } else {
+            if (o.f64) pool.widen_u8((double*)o.host + pt.off, (const uint8_t*)zp, pt.n);
+            else pool.copy((uint8_t*)o.host + pt.off, zp, pt.n);
+        }
+        ht.acc[1] += t1 - t0;
+        ht.acc[2] += ht.now_us() - t1;
+    }
+    return RSP_OK;
+}
+
+static int host_chain_small(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
+                            int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout,
+                            void* flag_out, void* flagV_out, bool f64, HostTrace& ht) {
+    auto& h = ctx->hp;
+    const int64_t Ro = ctx->p.R_out, V = ctx->V, beams = ctx->beams;
+    const bool narrow = dtype == RSP_C128;
+    const int32_t ddtype = narrow ? RSP_C64 : dtype;
+    const size_t ein = dtype_size(dtype), edev = dtype_size(ddtype);
+    const bool conv = layout != RSP_ROWMAJOR, tr = out_layout == RSP_COLMAJOR;
+    const bool want_fv = cfar && flagV_out;
+    const int64_t planes = batch * beams;
+    const size_t elems = (size_t)planes * P * R, dbytes = elems * edev;
+    const size_t cells = (size_t)V * Ro, ocells = (size_t)batch * cells;
+    const int nkinds = (rdm_out ? 1 : 0) + (cfar ? 1 : 0) + (want_fv ? 1 : 0);
+    if (dbytes > kZcMaxIn || (int64_t)nkinds * batch > h.kParts || (!tr && (ocells % 4) != 0) ||
+        (!conv && (dbytes % 4) != 0))
+        return RSP_ERR_UNSUPPORTED;   // (the DMA pipeline takes it; no error text)
+    int rc;
+    if ((rc = zc_ensure(ctx, &h.zc_in, &h.zc_in_n, dbytes))) return rc;
+    if ((rc = ensure(ctx, h.in[0], dbytes))) return rc;
+    if (conv && (rc = ensure(ctx, h.canon[0], elems * sizeof(float2)))) return rc;
+    if ((rc = ensure(ctx, h.rdm[0], ocells * sizeof(float)))) return rc;
+    if (cfar && (rc = ensure(ctx, h.flag[0], ocells))) return rc;
+    if (want_fv && (rc = ensure(ctx, h.flagV[0], ocells))) return rc;
+    rsp::CopyPool& pool = host_pool(ctx);
+    hipStream_t st = ctx->stream;
+    char* zin = (char*)h.zc_in;
+    const char* src = (const char*)echo;
+    // ---- input pieces: source elements [s0, s0 + n)
+    auto stage = [&](size_t s0, size_t n) {
+        const double t0 = ht.now_us();
+        if (narrow) pool.narrow_c128((float*)(zin + s0 * edev), (const double*)(src + s0 * ein), n);
+        else pool.copy(zin + s0 * edev, src + s0 * ein, n * edev);
+        std::atomic_thread_fence(std::memory_order_release);
+        ht.acc[0] += ht.now_us() - t0;
+    };
+    static const size_t kPiece = (size_t)zc_knob("RSP_ZC_PIECE_KIB", (int)(kZcPiece >> 10)) << 10;
+    if (conv) {   // plane k = [R][P] -> canon [P][R]; a piece = rows [r0, r1) of one plane
+        int64_t rp = (int64_t)(kPiece / ((size_t)P * edev)) / 32 * 32;
+        if (rp < 32) rp = 32;
+        const int elem = ddtype == RSP_C32F16 ? rsp::RSP_SUB_C32F16 : rsp::RSP_SUB_C64;
+        for (int64_t k = 0; k < planes; ++k)
+            for (int64_t r0 = 0; r0 < R; r0 += rp) {
+                const int64_t r1 = r0 + rp < R ? r0 + rp : R;
+                const size_t s0 = (size_t)(k * R + r0) * P;
+                stage(s0, (size_t)(r1 - r0) * P);
+                HIP_TRY(ctx, rsp::launch_transpose_sub(elem, zin + s0 * edev,
+                                                       (float2*)h.canon[0].p + (size_t)k * P * R + r0, (int)(r1 - r0),
+                                                       (int)P, (size_t)P, (size_t)R, st));
+            }
+    } else {      // row-major: contiguous pieces, copied as they are
+        const size_t pe = (kPiece / edev + 1023) / 1024 * 1024;
+        for (size_t s0 = 0; s0 < elems; s0 += pe) {
+            const size_t n = elems - s0 < pe ? elems - s0 : pe;
+            stage(s0, n);
+            HIP_TRY(ctx, rsp::launch_copy_words(zin + s0 * edev, (char*)h.in[0].p + s0 * edev, n * edev / 4, st));
+        }
+    }
+    ht.mark();   // 2: input staged
+    ht.ev(2, st);
+    int rc2 = rsp_pc_mtd_cfar_dev(ctx, conv ? h.canon[0].p : h.in[0].p, conv ? RSP_C64 : ddtype, batch, cfar,
+                                  (float*)h.rdm[0].p, cfar ? (uint8_t*)h.flag[0].p : nullptr,
+                                  want_fv ? (uint8_t*)h.flagV[0].p : nullptr, st);
+    if (rc2) return rc2;
+    ht.ev(3, st);
+    ht.ev(4, st);
+    ZcOut outs[3];
+    int no = 0;
+    if (rdm_out) outs[no++] = {h.rdm[0].p, 4, rdm_out, f64};
+    if (cfar) outs[no++] = {h.flag[0].p, 1, flag_out, f64};
+    if (want_fv) outs[no++] = {h.flagV[0].p, 1, flagV_out, f64};
+    if ((rc = zc_deliver(ctx, outs, no, batch, V, Ro, tr, ht))) return rc;
+    ht.ev(5, st);
+    ht.mark();   // 4: outputs delivered
+    return RSP_OK;
 }
 
 static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
@@ -1707,6 +1924,30 @@ static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t lay
     if (K < 1) K = 1;
     if (K > batch) K = batch;
     const int64_t nk = (batch + K - 1) / K;
+    if (nk == 1 && zc_mode() != 0) {
+        ht.mark();   // 1: set up
+        rc = host_chain_small(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out,
+                              f64, ht);
+        if (rc != RSP_ERR_UNSUPPORTED) {
+            if (rc == RSP_OK && ht.on) {
+                ht.mark();   // 5
+                (void)hipStreamSynchronize(ctx->stream);
+                float g[2] = {};
+                (void)hipEventElapsedTime(&g[0], ht.e[2], ht.e[3]);
+                (void)hipEventElapsedTime(&g[1], ht.e[4], ht.e[5]);
+                auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(ht.t[b] - ht.t[a]).count(); };
+                fprintf(stderr, "rsp_host_trace batch %lld chunks 1 zc host_us setup %.1f stage_in %.1f enqueue %.1f "
+                        "stage_out %.1f sync %.1f total %.1f dev_us h2d 0 chain %.1f d2h %.1f zc_us narrow %.1f "
+                        "wait %.1f widen %.1f\n", (long long)batch,
+                        us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(0, 5), g[0] * 1e3, g[1] * 1e3, ht.acc[0],
+                        ht.acc[1], ht.acc[2]);
+            }
+            if (ht.on)
+                for (auto& e : ht.e) (void)hipEventDestroy(e);
+            return rc;
+        }
+        ht.n = 1;   // (the DMA pipeline's marks follow)
+    }
     for (int i = 0; i < h.kSlots && i < nk; ++i) {
         if ((rc = ensure(ctx, h.in[i], (size_t)K * dev_cpi))) return rc;
         if (conv && (rc = ensure(ctx, h.canon[i], (size_t)K * beams * P * R * sizeof(float2)))) return rc;
@@ -1858,11 +2099,48 @@ static int cfar_f64_body(rsp_ctx* ctx, const double* rdm, int32_t rdm_layout, in
     if ((rc = ensure(ctx, ctx->st_flag, cells))) return rc;
     if ((rc = ensure(ctx, ctx->st_flagV, cells))) return rc;
     auto& h = ctx->hp;
+    const bool col = rdm_layout == RSP_COLMAJOR;
+    if (zc_mode() != 0 && cells * sizeof(float) <= kZcMaxIn && (flagV_out ? 2 : 1) * batch <= h.kParts &&
+        (col || cells % 4 == 0)) {
+        // one chunk (executeCFAR's segments): the narrowed pieces are read from pinned staging by
+        // the transpose / copy kernels, the flags written back into it part by part (host_chain_small)
+        if ((rc = zc_ensure(ctx, &h.zc_in, &h.zc_in_n, cells * sizeof(float)))) return rc;
+        rsp::CopyPool& pool = host_pool(ctx);
+        char* zin = (char*)h.zc_in;
+        hipStream_t st = ctx->stream;
+        if (col) {   // plane k = [R][V] -> [V][R]; a piece = rows [r0, r1) of one plane
+            int64_t rp = (int64_t)(kZcPiece / ((size_t)V * sizeof(float))) / 32 * 32;
+            if (rp < 32) rp = 32;
+            for (int64_t k = 0; k < batch; ++k)
+                for (int64_t r0 = 0; r0 < R; r0 += rp) {
+                    const int64_t r1 = r0 + rp < R ? r0 + rp : R;
+                    const size_t s0 = (size_t)(k * R + r0) * V;
+                    pool.narrow_f64((float*)zin + s0, rdm + s0, (size_t)(r1 - r0) * V);
+                    std::atomic_thread_fence(std::memory_order_release);
+                    HIP_TRY(ctx, rsp::launch_transpose_sub(rsp::RSP_SUB_F32, (float*)zin + s0,
+                                                           (float*)ctx->st_rdm.p + (size_t)k * V * R + r0, (int)(r1 - r0),
+                                                           (int)V, (size_t)V, (size_t)R, st));
+                }
+        } else {
+            const size_t pe = kZcPiece / sizeof(float);
+            for (size_t s0 = 0; s0 < cells; s0 += pe) {
+                const size_t n = cells - s0 < pe ? cells - s0 : pe;
+                pool.narrow_f64((float*)zin + s0, rdm + s0, n);
+                std::atomic_thread_fence(std::memory_order_release);
+                HIP_TRY(ctx, rsp::launch_copy_words((float*)zin + s0, (float*)ctx->st_in.p + s0, n, st));
+            }
+        }
+        rc = rsp_cfar_dev(ctx, (const float*)(col ? ctx->st_rdm.p : ctx->st_in.p), V, R, batch, cfar,
+                          (uint8_t*)ctx->st_flag.p, (uint8_t*)ctx->st_flagV.p, st);
+        if (rc) return rc;
+        ZcOut outs[2] = {{ctx->st_flag.p, 1, flag_out, true}, {ctx->st_flagV.p, 1, flagV_out, true}};
+        HostTrace none;
+        return zc_deliver(ctx, outs, flagV_out ? 2 : 1, batch, V, R, col, none);
+    }
     if ((rc = h2d_pieces(ctx, ctx->st_in.p, rdm, cells * sizeof(float), 2))) return rc;
     HIP_TRY(ctx, hipEventRecord(h.ev_in[0], h.s_h2d));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, h.ev_in[0], 0));
     const float* d_rdm = (const float*)ctx->st_in.p;
-    const bool col = rdm_layout == RSP_COLMAJOR;
     if (col) {  // MATLAB V x R = [b][R][V] -> [b][V][R]
         HIP_TRY(ctx, rsp::launch_transpose_f32(d_rdm, (float*)ctx->st_rdm.p, batch, (int)R, (int)V, ctx->stream));
         d_rdm = (const float*)ctx->st_rdm.p;

@@ -3,7 +3,18 @@
 // for the pageable <-> pinned staging copies.  One memcpy thread moves 20-30 GB/s of host DRAM,
 // 8 threads ~130 GB/s (profiles/r04/probe1/pcie_probe.txt), against ~57 GB/s of PCIe Gen5 DMA
 // per direction, so each staging piece is split over the pool.
+//
+// A one-CPI call (the MEX granularity) runs the pool ~8 times for ~1 MiB each, so the hand-off
+// itself is on the critical path: a condition-variable wake costs several microseconds per
+// worker.  Workers therefore spin on the job generation for kSpinUs after their last part before
+// they block, and the caller spins on the pending count while the parts run.  The conversions
+// write with streaming (non-temporal) stores: the destination -- pinned staging or the caller's
+// fresh output array -- is not read back by this thread, so the store skips the cache line fill.
 #pragma once
+#include <emmintrin.h>
+
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -39,29 +50,42 @@ public:
     }
 
     // complex double -> complex float (MATLAB's C128 echo -> the chain's C64), `n` complex
-    // samples: the (float) casts round to nearest-even exactly as the GPU's v_cvt_f32_f64, so the
-    // chain sees the same samples as when it converts on the device.
+    // samples: cvtpd2ps rounds to nearest-even under the default MXCSR exactly as the (float)
+    // cast (cvtsd2ss) and the GPU's v_cvt_f32_f64, so the chain sees the same samples as when it
+    // converts on the device.
     void narrow_c128(float* dst, const double* src, size_t n) {
-        run(n, 512, [=](size_t a, size_t b) {
-            for (size_t i = 2 * a; i < 2 * b; ++i) dst[i] = (float)src[i];
-        });
+        run(n, 512, [=](size_t a, size_t b) { narrow_nt(dst + 2 * a, src + 2 * a, 2 * (b - a)); });
     }
 
     // MATLAB's output types: float RDM cells and 0/1 flag bytes widened to double (exact), and
     // a real double input narrowed to float (round to nearest, as the (float) cast on the GPU)
     void widen_f32(double* dst, const float* src, size_t n) {
         run(n, 1024, [=](size_t a, size_t b) {
-            for (size_t i = a; i < b; ++i) dst[i] = (double)src[i];
+            double* d = dst + a;
+            const float* s = src + a;
+            size_t m = b - a, i = 0;
+            for (; i < m && ((uintptr_t)(d + i) & 15u) != 0; ++i) d[i] = (double)s[i];
+            for (; i + 4 <= m; i += 4) {
+                const __m128 v = _mm_loadu_ps(s + i);
+                _mm_stream_pd(d + i, _mm_cvtps_pd(v));
+                _mm_stream_pd(d + i + 2, _mm_cvtps_pd(_mm_movehl_ps(v, v)));
+            }
+            for (; i < m; ++i) d[i] = (double)s[i];
+            _mm_sfence();
         });
     }
     void narrow_f64(float* dst, const double* src, size_t n) {
-        run(n, 1024, [=](size_t a, size_t b) {
-            for (size_t i = a; i < b; ++i) dst[i] = (float)src[i];
-        });
+        run(n, 1024, [=](size_t a, size_t b) { narrow_nt(dst + a, src + a, b - a); });
     }
     void widen_u8(double* dst, const uint8_t* src, size_t n) {
         run(n, 4096, [=](size_t a, size_t b) {
-            for (size_t i = a; i < b; ++i) dst[i] = (double)src[i];
+            double* d = dst + a;
+            const uint8_t* s = src + a;
+            size_t m = b - a, i = 0;
+            for (; i < m && ((uintptr_t)(d + i) & 15u) != 0; ++i) d[i] = (double)s[i];
+            for (; i + 2 <= m; i += 2) _mm_stream_pd(d + i, _mm_set_pd((double)s[i + 1], (double)s[i]));
+            for (; i < m; ++i) d[i] = (double)s[i];
+            _mm_sfence();
         });
     }
 
@@ -73,26 +97,43 @@ public:
         }
         size_t per = (n + n_ - 1) / n_;
         per = (per + align - 1) / align * align;
+        fn_ = &fn;
+        n_items_ = n;
+        per_ = per;
+        pending_.store(n_ - 1, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> g(m_);
-            fn_ = &fn;
-            n_items_ = n;
-            per_ = per;
-            pending_ = n_ - 1;
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);   // publishes fn_ / n_items_ / per_
         }
-        cv_.notify_all();
+        if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
         part(0);
-        std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [this] { return pending_ == 0; });
+        for (unsigned spins = 0; pending_.load(std::memory_order_acquire) != 0; ++spins) {
+            _mm_pause();
+            if ((spins & 0xffffu) == 0xffffu) std::this_thread::yield();   // a descheduled worker
+        }
     }
 
 private:
     static constexpr int kMinSplit = 1 << 20;
+    static constexpr int kSpinUs = 200;   // workers spin this long after a part before blocking
+
+    // count doubles -> floats, streaming stores where the destination is 16-byte aligned
+    static void narrow_nt(float* d, const double* s, size_t m) {
+        size_t i = 0;
+        for (; i < m && ((uintptr_t)(d + i) & 15u) != 0; ++i) d[i] = (float)s[i];
+        for (; i + 4 <= m; i += 4) {
+            const __m128 lo = _mm_cvtpd_ps(_mm_loadu_pd(s + i));
+            const __m128 hi = _mm_cvtpd_ps(_mm_loadu_pd(s + i + 2));
+            _mm_stream_ps(d + i, _mm_movelh_ps(lo, hi));
+        }
+        for (; i < m; ++i) d[i] = (float)s[i];
+        _mm_sfence();
+    }
+
     void stop_all() {
         {
             std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
+            stop_.store(true, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto& w : workers_)
@@ -106,28 +147,39 @@ private:
         (*fn_)(a, b);
     }
     void loop(int i) {
+        // (generation 0, not the current value: a worker that starts after the first run() was
+        // published must still take that job)
         uint64_t seen = 0;
         for (;;) {
-            {
+            // spin phase: a new job usually follows within microseconds during a call
+            const auto t0 = std::chrono::steady_clock::now();
+            for (unsigned spins = 0; gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_acquire);
+                 ++spins) {
+                _mm_pause();
+                if ((spins & 255u) == 255u &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs))
+                    break;
+            }
+            if (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_acquire)) {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
+                sleepers_.fetch_add(1, std::memory_order_acq_rel);
+                cv_.wait(lk, [&] { return stop_.load(std::memory_order_acquire) || gen_.load(std::memory_order_acquire) != seen; });
+                sleepers_.fetch_sub(1, std::memory_order_acq_rel);
             }
+            if (stop_.load(std::memory_order_acquire)) return;
+            seen = gen_.load(std::memory_order_acquire);
             part(i);
-            {
-                std::lock_guard<std::mutex> g(m_);
-                if (--pending_ == 0) done_.notify_one();
-            }
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
         }
     }
     int n_;
     std::vector<std::thread> workers_;
     std::mutex m_;
-    std::condition_variable cv_, done_;
-    bool stop_ = false;
-    uint64_t gen_ = 0;
-    int pending_ = 0;
+    std::condition_variable cv_;
+    std::atomic<bool> stop_{false};
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<int> sleepers_{0};
     const std::function<void(size_t, size_t)>* fn_ = nullptr;
     size_t n_items_ = 0, per_ = 0;
 };

@@ -273,5 +273,13 @@ hipError_t launch_transpose_f32(const float* in, float* out, int64_t batch, int 
                                 hipStream_t s);
 hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, int A, int B,
                                hipStream_t s);
+// One plane's sub-block transpose: element (a, b), a < A, b < B, of in[a*in_pitch + b] to
+// out[b*out_pitch + a] (elements: RSP_SUB_*; C32F16 widens to complex float).  The host path's
+// pieces: either pointer may be pinned host memory.
+enum { RSP_SUB_F32 = 0, RSP_SUB_U8 = 1, RSP_SUB_C64 = 2, RSP_SUB_C32F16 = 3 };
+hipError_t launch_transpose_sub(int elem, const void* in, void* out, int A, int B, size_t in_pitch, size_t out_pitch,
+                                hipStream_t s);
+// nwords 4-byte words in -> out (either may be pinned host memory)
+hipError_t launch_copy_words(const void* in, void* out, size_t nwords, hipStream_t s);
 
 }  // namespace rsp

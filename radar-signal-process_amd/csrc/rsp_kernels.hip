@@ -2479,40 +2479,51 @@ __global__ __launch_bounds__(kBlock) void ingest_row_kernel(const TIn* __restric
         out[i] = ld_el(in + i);
 }
 
-// in [b][A][B] -> out [b][B][A] through a 32x33 LDS tile (element conversion on load)
+// in [b][A][B] -> out [b][B][A] through a 32x33 LDS tile (element conversion on load).  The
+// pitches make it a sub-block transpose: element (a, b) of plane k is in[k*in_plane + a*in_pitch + b]
+// and lands at out[k*out_plane + b*out_pitch + a] -- the whole-plane transpose is in_pitch = B,
+// out_pitch = A; the host path's pieces use a block of rows or columns of a plane (either side
+// may be pinned host memory: the one-CPI calls read their input from, and write their outputs
+// into, pinned staging directly).
 template <typename TIn, typename TOut>
-__global__ __launch_bounds__(kBlock) void transpose_kernel(const TIn* __restrict__ in,
-                                                           TOut* __restrict__ out, int A, int B) {
+__global__ __launch_bounds__(kBlock) void transpose_kernel(const TIn* __restrict__ in, TOut* __restrict__ out,
+                                                           int A, int B, size_t in_pitch, size_t out_pitch,
+                                                           size_t in_plane, size_t out_plane) {
     __shared__ TOut tile[32][33];
     const size_t b = blockIdx.y;
     const int tilesB = (B + 31) / 32;
     const int a0 = (blockIdx.x / tilesB) * 32, b0 = (blockIdx.x % tilesB) * 32;
     const int tx = threadIdx.x % 32, ty = threadIdx.x / 32;
-    const TIn* src = in + b * (size_t)A * B;
-    TOut* dst = out + b * (size_t)A * B;
+    const TIn* src = in + b * in_plane;
+    TOut* dst = out + b * out_plane;
     for (int k = ty; k < 32; k += kBlock / 32) {
         const int aa = a0 + k, bb = b0 + tx;
-        if (aa < A && bb < B) tile[k][tx] = ld_el(src + (size_t)aa * B + bb);
+        if (aa < A && bb < B) tile[k][tx] = ld_el(src + (size_t)aa * in_pitch + bb);
     }
     __syncthreads();
     for (int k = ty; k < 32; k += kBlock / 32) {
         const int bb = b0 + k, aa = a0 + tx;
-        if (aa < A && bb < B) dst[(size_t)bb * A + aa] = tile[tx][k];
+        if (aa < A && bb < B) dst[(size_t)bb * out_pitch + aa] = tile[tx][k];
     }
 }
 
 template <typename TIn, typename TOut>
-static hipError_t launch_transpose_t(const TIn* in, TOut* out, int64_t batch, int A, int B,
-                                     hipStream_t s) {
+static hipError_t launch_transpose_t(const TIn* in, TOut* out, int64_t batch, int A, int B, size_t in_pitch,
+                                     size_t out_pitch, size_t in_plane, size_t out_plane, hipStream_t s) {
     if (batch <= 0 || A <= 0 || B <= 0) return hipSuccess;
     const unsigned tiles = (unsigned)(((A + 31) / 32) * ((B + 31) / 32));
     for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
         const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
         dim3 grid(tiles, (unsigned)nb), block(kBlock);
-        hipLaunchKernelGGL((transpose_kernel<TIn, TOut>), grid, block, 0, s,
-                           in + b0 * (size_t)A * B, out + b0 * (size_t)A * B, A, B);
+        hipLaunchKernelGGL((transpose_kernel<TIn, TOut>), grid, block, 0, s, in + b0 * in_plane, out + b0 * out_plane,
+                           A, B, in_pitch, out_pitch, in_plane, out_plane);
     }
     return hipGetLastError();
+}
+template <typename TIn, typename TOut>
+static hipError_t launch_transpose_t(const TIn* in, TOut* out, int64_t batch, int A, int B, hipStream_t s) {
+    const size_t plane = (size_t)A * B;
+    return launch_transpose_t(in, out, batch, A, B, (size_t)B, (size_t)A, plane, plane, s);
 }
 
 hipError_t launch_ingest(const void* in, int dtype, int layout, float2* out, int64_t batch,
@@ -2548,6 +2559,43 @@ hipError_t launch_transpose_f32(const float* in, float* out, int64_t batch, int 
 hipError_t launch_transpose_u8(const uint8_t* in, uint8_t* out, int64_t batch, int A, int B,
                                hipStream_t s) {
     return launch_transpose_t(in, out, batch, A, B, s);
+}
+
+hipError_t launch_transpose_sub(int elem, const void* in, void* out, int A, int B, size_t in_pitch, size_t out_pitch,
+                                hipStream_t s) {
+    switch (elem) {
+        case RSP_SUB_F32:
+            return launch_transpose_t((const float*)in, (float*)out, 1, A, B, in_pitch, out_pitch, 0, 0, s);
+        case RSP_SUB_U8:
+            return launch_transpose_t((const uint8_t*)in, (uint8_t*)out, 1, A, B, in_pitch, out_pitch, 0, 0, s);
+        case RSP_SUB_C64:
+            return launch_transpose_t((const float2*)in, (float2*)out, 1, A, B, in_pitch, out_pitch, 0, 0, s);
+        case RSP_SUB_C32F16:
+            return launch_transpose_t((const __half2*)in, (float2*)out, 1, A, B, in_pitch, out_pitch, 0, 0, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// n 4-byte words from `in` to `out` (either may be pinned host memory), 16 bytes per lane
+// where both are 16-byte aligned
+__global__ __launch_bounds__(kBlock) void copy_words_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                            size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const size_t n4 = ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0) ? n / 4 : 0;
+    const uint4* in4 = reinterpret_cast<const uint4*>(in);
+    uint4* out4 = reinterpret_cast<uint4*>(out);
+    for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < n4; i += stride) out4[i] = in4[i];
+    for (size_t i = 4 * n4 + blockIdx.x * (size_t)kBlock + threadIdx.x; i < n; i += stride) out[i] = in[i];
+}
+
+hipError_t launch_copy_words(const void* in, void* out, size_t nwords, hipStream_t s) {
+    if (nwords == 0) return hipSuccess;
+    size_t blocks = (nwords / 4 + kBlock - 1) / kBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(copy_words_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint32_t*)in, (uint32_t*)out,
+                       nwords);
+    return hipGetLastError();
 }
 
 }  // namespace rsp

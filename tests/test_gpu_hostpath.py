@@ -166,3 +166,84 @@ def test_f64_entry_points_equal_float_forms(torch_cuda):
         assert np.array_equal(cf64, cf8.astype(np.float64)) and np.array_equal(cv64, cv8.astype(np.float64))
         assert cf64.sum() > 0
     eng.close()
+
+
+@pytest.mark.parametrize("P,R,batch", [(64, 1024, 1), (64, 1024, 6), (128, 4096, 1), (128, 4096, 3)])
+def test_one_chunk_calls_stage_through_pinned_memory(torch_cuda, P, R, batch):
+    """A call whose batch fits one chunk (the MEX granularity) runs the one-chunk path: the
+    ingest transposes / copies read the echo from pinned staging piece by piece, and the output
+    transposes / copies write pinned staging part by part while the copy threads deliver earlier
+    parts.  Back-to-back calls with new inputs (the staging is reused: no stale lines), both
+    layouts, C128 / C64 / fp16 inputs, with and without flagV and CFAR, and the double outputs:
+    all bit-exact against the device path."""
+    torch = torch_cuda
+    import ctypes as C
+    from rsp import _capi as capi
+    from rsp import presets, synth
+    eng = _engine(P, R)
+    cf = presets.default_cfar(eng.spec)
+    eng.set_host_pipeline(0, 0)
+    V, Ro = eng.shape
+    for seed in (11, 12, 13):
+        echo = synth.echo_numpy(eng.spec, batch, seed=seed * 10 + batch).astype(np.complex64)
+        want = _dev(torch, eng, echo, cf)
+        col = np.ascontiguousarray(np.swapaxes(echo.astype(np.complex128), 1, 2))
+        got = eng.pc_mtd_cfar(col, cf, layout=capi.RSP_COLMAJOR, out_layout=capi.RSP_COLMAJOR)
+        for g, w in zip(got, want):
+            assert np.array_equal(np.swapaxes(g, 1, 2), w)
+        got = eng.pc_mtd_cfar(echo, cf)   # row-major C64 in and out
+        for g, w in zip(got, want):
+            assert np.array_equal(g, w)
+        rdm, flag, fv = eng.pc_mtd_cfar(col, cf, layout=capi.RSP_COLMAJOR, want_flagV=False)
+        assert fv is None and np.array_equal(rdm, want[0]) and np.array_equal(flag, want[1])
+        assert np.array_equal(eng.pc_mtd(echo), want[0])
+    # MATLAB's double outputs (the fun_MTD_produce shim's call), column-major
+    lib = eng.lib
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    r64 = np.full((batch, Ro, V), np.nan)
+    assert lib.rsp_pc_mtd_cfar_f64(eng.ctx, ptr(col), capi.RSP_C128, capi.RSP_COLMAJOR, P, R, batch, None, ptr(r64),
+                                   capi.RSP_COLMAJOR, None, None) == 0
+    assert np.array_equal(np.swapaxes(r64, 1, 2), want[0].astype(np.float64))
+    # fp16 I/Q, column-major ([b][R][P] of half2) and row-major
+    iq = np.stack([echo.real, echo.imag], axis=-1).astype(np.float16)   # [b, P, R, 2]
+    rdm = torch.empty((batch, V, Ro), dtype=torch.float32, device="cuda")
+    flag = torch.empty((batch, V, Ro), dtype=torch.uint8, device="cuda")
+    eng.run_dev(torch.from_numpy(np.ascontiguousarray(iq)).cuda(), rdm=rdm, flag=flag, cfar=cf)
+    torch.cuda.synchronize()
+    w16 = (rdm.cpu().numpy(), flag.cpu().numpy())
+    got = eng.pc_mtd_cfar(np.ascontiguousarray(iq), cf, want_flagV=False)
+    assert np.array_equal(got[0], w16[0]) and np.array_equal(got[1], w16[1])
+    iqc = np.ascontiguousarray(np.swapaxes(iq, 1, 2))                    # [b, R, P, 2]
+    got = eng.pc_mtd_cfar(iqc, cf, layout=capi.RSP_COLMAJOR, want_flagV=False)
+    assert np.array_equal(got[0], w16[0]) and np.array_equal(got[1], w16[1])
+    eng.close()
+
+
+def test_one_chunk_two_beam(torch_cuda):
+    """The one-chunk path with a two-beam (DMX) context: batch * beams input planes."""
+    torch = torch_cuda
+    from rsp import _capi as capi
+    from rsp import presets
+    from rsp.engine import Engine
+    spec = presets.dmx_native()
+    eng = Engine(spec, device=0)
+    cf = presets.dmx_native_cfar(spec)
+    eng.set_host_pipeline(0, 0)
+    B = 1
+    rng = np.random.default_rng(5151)
+    e = ((rng.standard_normal((B, 2, spec.P, spec.R)) + 1j * rng.standard_normal((B, 2, spec.P, spec.R)))
+         * np.sqrt(0.5)).astype(np.complex64)
+    V, Ro = eng.shape
+    rdm = torch.empty((B, V, Ro), dtype=torch.float32, device="cuda")
+    flag = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+    fv = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+    eng.run_dev(torch.from_numpy(e).cuda(), rdm=rdm, flag=flag, flagV=fv, cfar=cf)
+    torch.cuda.synchronize()
+    want = (rdm.cpu().numpy(), flag.cpu().numpy(), fv.cpu().numpy())
+    col = np.ascontiguousarray(np.swapaxes(e.astype(np.complex128), 2, 3))
+    got = eng.pc_mtd_cfar(col, cf, layout=capi.RSP_COLMAJOR)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    rdm2, flag2, _ = eng.pc_mtd_cfar(e, cf, want_flagV=False)
+    assert np.array_equal(rdm2, want[0]) and np.array_equal(flag2, want[1])
+    eng.close()

@@ -1,0 +1,36 @@
+"""The host copy pool of the host-buffer path (radar-signal-process_amd/csrc/rsp_hostpool.h:
+spin-then-block job hand-off, streaming-store conversions) on the CPU: every conversion equals
+the scalar cast over thread counts, split sizes and misaligned destinations, and a
+ThreadSanitizer build of the same check reports no race (when the toolchain has TSan)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "native", "hostpool_check.cpp")
+INC = os.path.join(ROOT, "radar-signal-process_amd", "csrc")
+
+
+def _build(tmp_path, name, extra):
+    exe = str(tmp_path / name)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-pthread", "-I", INC, SRC, "-o", exe] + extra, check=True,
+                   capture_output=True, text=True, timeout=300)
+    return exe
+
+
+def test_copy_pool_conversions_match_scalar_casts(tmp_path):
+    exe = _build(tmp_path, "hostpool_check", [])
+    r = subprocess.run([exe, "20"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
+
+
+def test_copy_pool_has_no_data_race_under_tsan(tmp_path):
+    try:
+        exe = _build(tmp_path, "hostpool_tsan", ["-fsanitize=thread", "-g"])
+    except subprocess.CalledProcessError as e:
+        pytest.skip("no ThreadSanitizer in this toolchain: %s" % e.stderr[-300:])
+    r = subprocess.run([exe, "2"], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0 and "FATAL: ThreadSanitizer" in r.stderr:
+        pytest.skip("ThreadSanitizer cannot run here: %s" % r.stderr[-300:])
+    assert r.returncode == 0 and "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-3000:]

@@ -14,7 +14,7 @@ once (MATLAB's own slicing is not the shim's cost).  With --compare, the round-4
 (lib*_mex_r4.so, built from commit f50fb2c's sources: float / byte outputs widened by a serial
 loop in the shim) run interleaved with the current ones, and their outputs must be identical.
 
-    python tools/mex_bench.py [--P 128 --R 4096] [--seconds 3] [--compare] [--json out.json]
+    python tools/mex_bench.py [--P 128 --R 4096] [--seconds 3] [--compare [--reps 3]] [--json out.json]
 """
 import argparse
 import ctypes as C
@@ -89,52 +89,68 @@ def v2_params(P, R):
             "point_prt": np.array([[R, 228, 723, R - 951]], dtype=np.float64)}
 
 
-def run(P=128, R=4096, seconds=3.0, compare=False):
+def run(P=128, R=4096, seconds=3.0, compare=False, reps=1):
+    """Each leg `reps` times, the shims alternating (current, r4, current, r4, ...), so drift of
+    the box's state hits both; the median rate is reported."""
     from rsp import presets, synth
     spec = presets.v2(P, R)
     echoes = synth.echo_numpy(spec, 4, seed=31).astype(np.complex128)
     names = ["current"] + (["r4"] if compare else [])
     files = {"current": "lib%s_mex.so", "r4": "lib%s_mex_r4.so"}
-    out = {"shape": [P, R], "seconds_per_leg": seconds, "fun_MTD_produce": {}, "executeCFAR": {}}
+    out = {"shape": [P, R], "seconds_per_leg": seconds, "reps": reps, "fun_MTD_produce": {}, "executeCFAR": {}}
     ref = {}
-    for nm in names:
-        sh = Shim(os.path.join(BUILD, files[nm] % "fun_MTD_produce"))
-        args = [[sh.arg(e), sh.arg(v2_params(P, R))] for e in echoes]
-        i = [0]
+    mtd = {nm: Shim(os.path.join(BUILD, files[nm] % "fun_MTD_produce")) for nm in names}
+    margs = {nm: [[sh.arg(e), sh.arg(v2_params(P, R))] for e in echoes] for nm, sh in mtd.items()}
+    rates = {nm: [] for nm in names}
+    for _ in range(reps):
+        for nm in names:
+            sh, args, i = mtd[nm], margs[nm], [0]
 
-        def one():
-            sh.call(1, args[i[0] % len(args)])
-            i[0] += 1
-        r, n = rate(one, seconds)
-        p = sh.call(1, args[0], keep=True)[0]
+            def one():
+                sh.call(1, args[i[0] % len(args)])
+                i[0] += 1
+            rates[nm].append(rate(one, seconds)[0])
+    for nm in names:
+        sh = mtd[nm]
+        p = sh.call(1, margs[nm][0], keep=True)[0]
         ref.setdefault("mtd", {})[nm] = sh.data(p, P * R)
         sh.lib.rt_free(p)
-        out["fun_MTD_produce"][nm] = {"calls_per_s": round(r, 1), "calls": n}
-        for a in args:
+        out["fun_MTD_produce"][nm] = {"calls_per_s": round(float(np.median(rates[nm])), 1),
+                                      "runs": [round(r, 1) for r in rates[nm]]}
+        for a in margs[nm]:
             for x in a:
                 sh.lib.rt_free(x)
     # executeCFAR on the chain's own RDM, per fun_CFARflag segment (v2 CFAR segments) and whole
     rdm = ref["mtd"]["current"].reshape((P, R), order="F")
     cf = presets.default_cfar(spec)
     segs = [(a, b) for a, b in cf.segments]
-    for nm in names:
-        sh = Shim(os.path.join(BUILD, files[nm] % "executeCFAR"))
-        scal = [5, 7, cf.TR, 0, 5, 7, cf.TV, 0, cf.M0, 1]
-        seg_args = [[sh.arg(np.ascontiguousarray(rdm[:, a:b]))] + [sh.arg(float(v)) for v in scal] for a, b in segs]
-        whole = [sh.arg(rdm)] + [sh.arg(float(v)) for v in scal]
+    scal = [5, 7, cf.TR, 0, 5, 7, cf.TV, 0, cf.M0, 1]
+    cfs = {nm: Shim(os.path.join(BUILD, files[nm] % "executeCFAR")) for nm in names}
+    sargs = {nm: [[sh.arg(np.ascontiguousarray(rdm[:, a:b]))] + [sh.arg(float(v)) for v in scal] for a, b in segs]
+             for nm, sh in cfs.items()}
+    wargs = {nm: [sh.arg(rdm)] + [sh.arg(float(v)) for v in scal] for nm, sh in cfs.items()}
+    fr = {nm: [] for nm in names}
+    wr = {nm: [] for nm in names}
+    for _ in range(reps):
+        for nm in names:
+            sh = cfs[nm]
 
-        def frame():
-            for a in seg_args:
-                sh.call(2, a)
-        r, n = rate(frame, seconds)
-        rw, nw = rate(lambda: sh.call(2, whole), seconds)
-        f = sh.call(2, whole, keep=True)
+            def frame():
+                for a in sargs[nm]:
+                    sh.call(2, a)
+            fr[nm].append(rate(frame, seconds)[0])
+            wr[nm].append(rate(lambda: sh.call(2, wargs[nm]), seconds)[0])
+    for nm in names:
+        sh = cfs[nm]
+        f = sh.call(2, wargs[nm], keep=True)
         ref.setdefault("cfar", {})[nm] = np.concatenate([sh.data(p, P * R) for p in f])
         for p in f:
             sh.lib.rt_free(p)
-        out["executeCFAR"][nm] = {"frames_per_s": round(r, 1), "segment_calls_per_frame": len(segs),
-                                  "whole_rdm_calls_per_s": round(rw, 1)}
-        for a in seg_args + [whole]:
+        out["executeCFAR"][nm] = {"frames_per_s": round(float(np.median(fr[nm])), 1),
+                                  "segment_calls_per_frame": len(segs),
+                                  "whole_rdm_calls_per_s": round(float(np.median(wr[nm])), 1),
+                                  "frame_runs": [round(r, 1) for r in fr[nm]]}
+        for a in sargs[nm] + [wargs[nm]]:
             for x in a:
                 sh.lib.rt_free(x)
     if compare:
@@ -153,13 +169,14 @@ def main():
     ap.add_argument("--R", type=int, default=4096)
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--compare", action="store_true")
+    ap.add_argument("--reps", type=int, default=1, help="legs per shim, alternating (median reported)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--trace", action="store_true",
                     help="RSP_HOST_TRACE=1: the library prints a per-call phase breakdown on stderr")
     a = ap.parse_args()
     if a.trace:
         os.environ["RSP_HOST_TRACE"] = "1"
-    out = run(a.P, a.R, a.seconds, a.compare)
+    out = run(a.P, a.R, a.seconds, a.compare, a.reps)
     print(json.dumps(out))
     if a.json:
         with open(a.json, "w") as f:
