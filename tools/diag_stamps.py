@@ -11,7 +11,8 @@ job done, 7 tail hits + all stores done (waited).  Slots 8/9: 100 MHz clock at e
 A waited boundary ends overlap that the real kernel has, so read the phases as a breakdown,
 not as the kernel's time.
 
-Usage: RSP_LIB=... python tools/diag_stamps.py [--cpis 16] [--json out.json]
+Usage: RSP_LIB=... python tools/diag_stamps.py [--config c3|c5] [--cpis 16] [--json out.json]
+(c5: 512 x 16384 fp16, the 16384-point segment as 5 overlap-save blocks of 4096, 16-bin MTD tiles)
 """
 import argparse
 import ctypes as C
@@ -59,24 +60,27 @@ def summarize(st, phases, sel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cpis", type=int, default=16)
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"])
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     import torch
     from rsp import presets, synth
     from rsp.engine import Engine
-    spec = presets.v2(128, 4096)
+    # (P, R, fp16 input, overlap-save blocks of the long segment, MTD tile width)
+    P, R, half, nsub, W = {"c3": (128, 4096, False, 1, 32), "c5": (512, 16384, True, 5, 16)}[args.config]
+    spec = presets.v2(P, R)
     cf = presets.default_cfar(spec)
     n = args.cpis
     eng = Engine(spec, chunk=n, streams=1)
     lib = eng.lib
     lib.rsp_diag_stamps.restype = C.c_int
     lib.rsp_diag_stamps.argtypes = [C.c_int, C.POINTER(C.c_uint64), C.c_int64]
-    echo = synth.echo_torch(spec, 2 * n, seed=3)
+    echo = synth.echo_torch(spec, 2 * n, seed=3, half=half)
     pc = torch.empty((2 * n, spec.P, spec.R_out), dtype=torch.complex64, device="cuda")
     for _ in range(3):
         eng.pc_dev(echo[:n], pc[:n])
     torch.cuda.synchronize()
-    nlong = n * spec.P                       # one 4096-point row per workgroup
+    nlong = n * spec.P * nsub                # one 4096-point row (block) per workgroup
     nshort = (n * spec.P + 3) // 4           # 4 rows of the 1024-point segment per workgroup
     st = read(lib, 0, nlong + nshort)
     res = {"pc_long_rows": summarize(st, PC_PHASES, slice(0, nlong)),
@@ -87,7 +91,7 @@ def main():
     for _ in range(3):
         eng.mtd_dev(pc, rdm=rdm, flag=flag, cfar=cf)
     torch.cuda.synchronize()
-    nm = n * (spec.R_out // 32)              # 32-bin tiles at P = 128
+    nm = n * ((spec.R_out + W - 1) // W)     # W-bin tiles
     st = read(lib, 1, nm)
     res["mtd_with_range_job"] = summarize(st, MTD_PHASES, slice(0, nm))
     print(json.dumps(res, indent=1))
