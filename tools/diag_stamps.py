@@ -12,7 +12,9 @@ A waited boundary ends overlap that the real kernel has, so read the phases as a
 not as the kernel's time.
 
 Usage: RSP_LIB=... python tools/diag_stamps.py [--config c3|c5] [--cpis 16] [--json out.json]
-(c5: 512 x 16384 fp16, the 16384-point segment as 5 overlap-save blocks of 4096, 16-bin MTD tiles)
+(c5: 512 x 16384 fp16, the 16384-point segment as 5 overlap-save blocks of 4096, 16-bin MTD tiles;
+c4: the c4 kernels -- 256-pulse MTD tiles of 16 bins, 8192-point rows as 3 blocks -- on plain
+256 x 8192 CPIs instead of sliding windows)
 """
 import argparse
 import ctypes as C
@@ -60,14 +62,15 @@ def summarize(st, phases, sel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cpis", type=int, default=16)
-    ap.add_argument("--config", default="c3", choices=["c3", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"])
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     import torch
     from rsp import presets, synth
     from rsp.engine import Engine
     # (P, R, fp16 input, overlap-save blocks of the long segment, MTD tile width)
-    P, R, half, nsub, W = {"c3": (128, 4096, False, 1, 32), "c5": (512, 16384, True, 5, 16)}[args.config]
+    P, R, half, nsub, W = {"c3": (128, 4096, False, 1, 32), "c4": (256, 8192, False, 3, 16),
+                           "c5": (512, 16384, True, 5, 16)}[args.config]
     spec = presets.v2(P, R)
     cf = presets.default_cfar(spec)
     n = args.cpis
