@@ -1280,16 +1280,6 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     }
 
     const auto dst = buf_rsrc(T.rdm, plane * 4u);
-    // (dev-only -DRSP_MTD_LDS_ROWS, A/B of VERDICT r4 item 3) with the Doppler CFAR on, the RDM
-    // leaves from the CFAR's staged magnitude columns instead of the registers: one 16-byte store
-    // per 4 columns of a row (a quarter of the store instructions, whole row segments per lane
-    // group) after one extra barrier
-#ifdef RSP_MTD_LDS_ROWS
-    constexpr bool kLdsRows = BEAMS == 1 && REF > 0 && W % 4 == 0;
-#else
-    constexpr bool kLdsRows = false;
-#endif
-    const bool lds_rows = kLdsRows && a.cv.enabled && (R % 4u) == 0u;
     const bool want_diff = BEAMS == 2 && T.diff != nullptr;
     const auto dfr = buf_rsrc(want_diff ? T.diff : nullptr, want_diff ? plane * 4u : 0u);
     const uint32_t vo_out = rv ? cell * 4u : kOob;
@@ -1305,10 +1295,8 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
             x += m0[m];                                                                      // |L| + |R|
         }
         mg[m] = x;
-        if (!lds_rows) {
-            if constexpr (SA != 0) buf_st_fa<SA>(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
-            else buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
-        }
+        if constexpr (SA != 0) buf_st_fa<SA>(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
+        else buf_st_f_stream(x, dst, vo_out, (uint32_t)(G * mm) * R * 4u);
     }
     // fun_0v_pressing's zeroed rows [z_lo, z_hi) (the DMX zeroSetFlagMTD band wraps through row
     // 0: rows [0, z_hi - P) too), as a second store of 0 to the few of the thread's rows inside
@@ -1320,10 +1308,8 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
         if constexpr (SA != 0) buf_st_fa<SA>(0.f, dst, vz, 0u);
         else buf_st_f_stream(0.f, dst, vz, 0u);
     };
-    if (!lds_rows) {
-        own_rows<G, E>(g, a.z_lo, a.z_hi, zero_rdm);
-        own_rows<G, E>(g, 0, zw, zero_rdm);
-    }
+    own_rows<G, E>(g, a.z_lo, a.z_hi, zero_rdm);
+    own_rows<G, E>(g, 0, zw, zero_rdm);
     RSP_STAMP(1, 3, false);
     if (!a.cv.enabled) return;
     lds_barrier();  // the FFT exchange slots are free from here on
@@ -1340,42 +1326,7 @@ __device__ __forceinline__ void mtd_tile(const MtdTile& T, const MtdArgs& a, uns
     auto zero_mag = [&](int mm) { mag[g + G * mm] = 0.f; };
     own_rows<G, E>(g, a.z_lo, a.z_hi, zero_mag);
     own_rows<G, E>(g, 0, zw, zero_mag);
-    if constexpr (kLdsRows) {
-        if (lds_rows) {
-            lds_barrier();   // the columns are staged (with the RDM's band zeroed)
-            // item (v, q): row v, columns 4q..4q+3 of the tile, from 4 staged columns; the same
-            // thread then writes the CFAR input's zero rows over the cells it read (main_cfar.m:90-91)
-            constexpr int QPR = W / 4;
-            float* col0 = reinterpret_cast<float*>(smem) + C::SPAD;
-            typedef int v4i __attribute__((ext_vector_type(4)));
-            for (int i = tx; i < P * QPR; i += C::T) {
-                const int v = i / QPR, q = i % QPR;
-                float* pc0 = col0 + (4 * q) * C::MS2 + v;
-                const float e0 = pc0[0], e1 = pc0[C::MS2], e2 = pc0[2 * C::MS2], e3 = pc0[3 * C::MS2];
-                const int c0 = T.bx * W + 4 * q;
-                const uint32_t off = ((uint32_t)v * R + (uint32_t)c0) * 4u;
-                if (c0 + 3 < (int)R) {
-                    __builtin_amdgcn_raw_buffer_store_b128(v4i{__builtin_bit_cast(int, e0), __builtin_bit_cast(int, e1),
-                                                               __builtin_bit_cast(int, e2), __builtin_bit_cast(int, e3)},
-                                                           dst, off, 0u, SA != 0 ? SA : kStreamAux);
-                } else {
-                    const float e[4] = {e0, e1, e2, e3};
-                    for (int j = 0; j < 4; ++j)
-                        if (c0 + j < (int)R) buf_st_fa<SA != 0 ? SA : kStreamAux>(e[j], dst, off + 4u * j, 0u);
-                }
-                if (v >= a.cv.cz_lo && v < a.cv.cz_hi) {
-                    pc0[0] = 0.f;
-                    pc0[C::MS2] = 0.f;
-                    pc0[2 * C::MS2] = 0.f;
-                    pc0[3 * C::MS2] = 0.f;
-                }
-            }
-        } else {
-            own_rows<G, E>(g, a.cv.cz_lo, a.cv.cz_hi, zero_mag);
-        }
-    } else {
-        own_rows<G, E>(g, a.cv.cz_lo, a.cv.cz_hi, zero_mag);
-    }
+    own_rows<G, E>(g, a.cv.cz_lo, a.cv.cz_hi, zero_mag);
     lds_barrier();
 
     const int v0 = cfar_run<G, W>(g) * E;   // this thread's run of Doppler rows
