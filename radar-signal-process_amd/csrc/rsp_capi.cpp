@@ -1818,8 +1818,9 @@ static int zc_deliver(rsp_ctx* ctx, const ZcOut* outs, int nout, int64_t batch, 
 
 static int host_chain_small(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
                             int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout,
-                            void* flag_out, void* flagV_out, bool f64, HostTrace& ht) {
+                            void* flag_out, void* flagV_out, bool f64, HostTrace& ht, bool& taken) {
     auto& h = ctx->hp;
+    taken = false;
     const int64_t Ro = ctx->p.R_out, V = ctx->V, beams = ctx->beams;
     const bool narrow = dtype == RSP_C128;
     const int32_t ddtype = narrow ? RSP_C64 : dtype;
@@ -1832,7 +1833,8 @@ static int host_chain_small(rsp_ctx* ctx, const void* echo, int32_t dtype, int32
     const int nkinds = (rdm_out ? 1 : 0) + (cfar ? 1 : 0) + (want_fv ? 1 : 0);
     if (dbytes > kZcMaxIn || (int64_t)nkinds * batch > h.kParts || (!tr && (ocells % 4) != 0) ||
         (!conv && (dbytes % 4) != 0))
-        return RSP_ERR_UNSUPPORTED;   // (the DMA pipeline takes it; no error text)
+        return RSP_OK;   // not taken: the DMA pipeline runs the call
+    taken = true;
     int rc;
     if ((rc = zc_ensure(ctx, &h.zc_in, &h.zc_in_n, dbytes))) return rc;
     if ((rc = ensure(ctx, h.in[0], dbytes))) return rc;
@@ -1926,9 +1928,10 @@ static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t lay
     const int64_t nk = (batch + K - 1) / K;
     if (nk == 1 && zc_mode() != 0) {
         ht.mark();   // 1: set up
+        bool taken = false;
         rc = host_chain_small(ctx, echo, dtype, layout, P, R, batch, cfar, rdm_out, out_layout, flag_out, flagV_out,
-                              f64, ht);
-        if (rc != RSP_ERR_UNSUPPORTED) {
+                              f64, ht, taken);
+        if (taken) {
             if (rc == RSP_OK && ht.on) {
                 ht.mark();   // 5
                 (void)hipStreamSynchronize(ctx->stream);
