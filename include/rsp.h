@@ -188,11 +188,14 @@ int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
 int rsp_set_streams(rsp_ctx* ctx, int32_t n);
 
 /* ---- host-buffer entry points (MEX / fun_MTD_produce drop-in), synchronous ---------- */
-/* rsp_pc_mtd_cfar / rsp_pc_mtd take pageable host buffers (MATLAB's arrays) and pipeline the
- * call in chunks of CPIs: chunk k's host->device copy, chain and device->host copy overlap
- * chunks k+1 and k-1 (two copy streams beside the context's stream); the pageable <-> pinned
- * staging runs through rings of 8 MiB pinned pieces copied by a host thread pool, so the copies
- * of one CPI also overlap their DMA.  Outputs are identical to the _dev path's. */
+/* rsp_pc_mtd_cfar / rsp_pc_mtd take pageable host buffers (MATLAB's arrays).  A call that fits
+ * one chunk (every MATLAB-granularity call) is staged through pinned memory that the kernels
+ * read and write directly across PCIe: the host copy threads convert ~1 MiB input pieces while
+ * the transpose kernels consume the earlier ones, and deliver ~1 MiB output parts while the later
+ * parts cross the link.  A larger batch is pipelined in chunks of CPIs: chunk k's host->device
+ * copy, chain and device->host copy overlap chunks k+1 and k-1 (two copy streams beside the
+ * context's stream), staged through rings of 8 MiB pinned pieces copied by the thread pool.
+ * Outputs are identical to the _dev path's. */
 /* CPIs per host chunk (0 = by size: 32 MiB of device-side input, 8 CPIs at 128 x 4096) and
  * host copy threads (0 = default: 8 with >= 16 hardware threads). */
 int rsp_set_host_pipeline(rsp_ctx* ctx, int64_t cpis_per_chunk, int32_t copy_threads);
@@ -213,7 +216,7 @@ int rsp_pc_mtd_cfar(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layou
  * MTD/fun_MTD_produce.m:12 and CFAR_WangCai/executeCFAR.m:1-2): as rsp_pc_mtd_cfar / rsp_cfar,
  * but the RDM and the 0/1 flags land as double and the CFAR input is double.  The widening
  * (float -> double, byte -> double) and narrowing (double -> float, round to nearest) run on
- * the host copy threads, piece by piece as each pinned piece's DMA lands, instead of in a
+ * the host copy threads, piece by piece as each pinned piece or part lands, instead of in a
  * serial loop in the shim.  Values are identical to the float / byte forms'.  rsp_pc_mtd_cfar_f64
  * with cfar == NULL is fun_MTD_produce. */
 int rsp_pc_mtd_cfar_f64(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout,
