@@ -1039,6 +1039,28 @@ static int run_flow(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncp
 // win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
 // frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
 // frames plus the look-ahead frame once, and every window reads its rows from that PC.
+// Where a chunk's range stage (executeCFAR's range test of the Doppler hits) runs:
+//   2 (default): grouped -- the range stages of up to kRangeGroup consecutive chunks of a lane run
+//     as one launch behind the group's last MTD; the MTD records hit indices relative to the
+//     group's first output cell (MtdArgs::cell_off).  Needs the caller's RDM (internal RDM slots
+//     are reused) and a group span inside the range kernels' 2 GiB buffer window.
+//   0: fused -- the stage rides in the next MTD launch on the lane (RangeJob57: gathers issued with
+//     the tile loads); the fallback when grouping does not apply.
+//   1: a standalone launch behind every chunk's MTD.
+// Measured (profiles/r05/ab/range_stage_grouping.txt): the fused job costs the MTD ~10 % at c3
+// even with 0.28 % hits; groups of 8-32 chunks: c3 +2 %, c5 +1.5-2.6 %, bit-identical; a launch
+// per chunk: c3 -1 %.  Dev A/B: environment RSP_RANGE_MODE / RSP_RANGE_GROUP (read once).
+static constexpr int kRangeGroup = 16;
+static constexpr uint64_t kRangeGroupBytes = 1ull << 30;   // hit-list slots of one call's groups
+static int range_mode() {
+    static const int m = [] { const char* v = getenv("RSP_RANGE_MODE"); return v && *v ? atoi(v) : 2; }();
+    return m;
+}
+static int range_group() {
+    static const int g = [] { const char* v = getenv("RSP_RANGE_GROUP"); const int x = v && *v ? atoi(v) : kRangeGroup; return x < 1 ? 1 : x; }();
+    return g;
+}
+
 static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
                           const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
                           float* d_diff, hipStream_t s, bool pc_input) {
@@ -1096,9 +1118,24 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         // two slots per lane: chunk k's list is read by the next MTD launch on its lane while
         // that launch fills the other slot
         rsp::mtd_regions((int)V, (int)Ro, (int)(cu * ocpi), &nreg, &reg, (int)NB);
-        rc = ensure(ctx, ctx->hit_list, (size_t)2 * ns * nreg * reg * sizeof(uint32_t));
+    }
+    // grouped range stages (range_mode 2): a group's outputs must stay inside the range kernels'
+    // 2 GiB buffer window, and the RDM must be the caller's (internal RDM slots are reused)
+    int rgrp = range_group();
+    if (cfar && nreg > 0) {   // the groups' hit-list slots within kRangeGroupBytes
+        const uint64_t slot_bytes = (uint64_t)nreg * (uint64_t)reg * 4u;
+        const uint64_t fit = kRangeGroupBytes / ((uint64_t)ns * slot_bytes);
+        if ((uint64_t)rgrp > fit) rgrp = fit > 0 ? (int)fit : 1;
+    }
+    const bool grouped = cfar && cr.rflag && d_rdm && range_mode() == 2 && rgrp > 1 &&
+                         ((uint64_t)(rgrp - 1) * (uint64_t)ns + 1u) * (uint64_t)cells * 4u < 0x80000000ull;   // (kOob, rsp_buf.h)
+    // hit-list slots per lane: grouped, a group's range launch is stream-ordered before the next
+    // group's first MTD on the lane, so the next group reuses the slots
+    const int spl = grouped ? rgrp : 2;
+    if (cfar) {
+        rc = ensure(ctx, ctx->hit_list, (size_t)spl * ns * nreg * reg * sizeof(uint32_t));
         if (rc) return rc;
-        rc = ensure(ctx, ctx->hit_ctr, (size_t)2 * ns * nreg * sizeof(uint32_t));
+        rc = ensure(ctx, ctx->hit_ctr, (size_t)spl * ns * nreg * sizeof(uint32_t));
         if (rc) return rc;
     }
     if (!d_rdm) {   // internal RDM: two slots per lane for the same reason
@@ -1138,10 +1175,13 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         const int64_t ncpi = n * ocpi;                     // CPIs this chunk produces
         const size_t o0 = (size_t)u0 * ocpi * plane;      // output offset
         const int lane = (int)(k % ns);
-        const int slot = lane * 2 + (int)((k / ns) & 1);   // double-buffered per lane
+        const int64_t j = k / ns;                          // the chunk's index on its lane
+        const int slot = lane * spl + (int)(j % spl);      // double-buffered per lane (grouped: one group)
+        const int64_t jg0 = j - j % rgrp;                  // grouped: the group's first chunk on the lane
+        const size_t og = grouped ? (size_t)cstart[(size_t)(lane + ns * jg0)] * ocpi * plane : o0;
         hipStream_t ls = lanes[lane];
         const char* ein = (const char*)d_echo + (size_t)u0 * NB * P * R * esz;
-        float* rdm = d_rdm ? d_rdm + o0 : (float*)ctx->tmp_rdm.p + slot * cells;
+        float* rdm = d_rdm ? d_rdm + o0 : (float*)ctx->tmp_rdm.p + (lane * 2 + (int)(j & 1)) * cells;
         uint8_t* fv = (cfar && d_flagV) ? d_flagV + o0 : nullptr;
         float2* pcs;
         if (pc_input) {   // d_echo already holds pulse-compressed rows [units][beams][P][R_out]
@@ -1152,13 +1192,14 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         }
         m.diff = d_diff ? d_diff + o0 : nullptr;
         m.prev_nregions = 0;
+        m.cell_off = (uint32_t)(o0 - og);   // hit indices relative to the group's first cell (else 0)
         if (cfar) {
             m.flag = d_flag + o0;
             m.rflag = cr.rflag;
             m.hits = (uint32_t*)ctx->hit_list.p + (size_t)slot * nreg * reg;
             m.hit_count = (uint32_t*)ctx->hit_ctr.p + (size_t)slot * nreg;
             const Pending& pv = pend[lane];
-            if (pv.nreg > 0) {
+            if (pv.nreg > 0 && !grouped) {
                 m.prev_rdm = pv.rdm;
                 m.prev_flag = pv.flag;
                 m.prev_hits = pv.hits;
@@ -1176,6 +1217,23 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
             pv.flag = m.flag;
             pv.hits = m.hits;
             pv.counts = m.hit_count;
+            if (grouped) {   // the group's range stages, one launch behind its last MTD
+                const bool last = k + ns >= nchunks;
+                if (j % rgrp == rgrp - 1 || last) {
+                    const int s0 = lane * spl + (int)(jg0 % spl);
+                    const int nr = (int)(j - jg0) * nreg + pv.nreg;   // full chunks, then this one's regions
+                    HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] {
+                        return rsp::launch_cfar_hits(d_rdm + og, d_flag + og, (uint32_t*)ctx->hit_list.p + (size_t)s0 * nreg * reg,
+                                                     (uint32_t*)ctx->hit_ctr.p + (size_t)s0 * nreg, nr, pv.reg, cr, ls);
+                    }));
+                }
+                pv.nreg = 0;
+            } else if (range_mode() == 1) {   // (dev A/B) the chunk's range stage as its own launch, now
+                HIP_TRY(ctx, timed(ctx, RSP_K_CFAR_R, ls, [&] {
+                    return rsp::launch_cfar_hits(pv.rdm, pv.flag, pv.hits, pv.counts, pv.nreg, pv.reg, cr, ls);
+                }));
+                pv.nreg = 0;
+            }
         }
     }
     for (int lane = 0; lane < ns; ++lane) {   // each lane's last chunk

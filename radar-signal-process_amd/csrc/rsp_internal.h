@@ -138,6 +138,7 @@ struct MtdArgs {
     int flag_zero;         // rflag: the MTD kernel writes the flag plane's zeros (else the host memsets it)
     uint32_t* hits;        // workgroup b owns hits[b*W*P, (b+1)*W*P) (its own cells: no overflow)
     uint32_t* hit_count;   // hit_count[b] = entries of workgroup b (b = blockIdx.y*gridDim.x + blockIdx.x)
+    uint32_t cell_off;     // added to every hit index (grouped range stages: the chunk's offset in its group)
     // The previous chunk's range stage, run by extra workgroups of this launch (same stream,
     // so that chunk's RDM and hit lists are complete): prev_nregions == 0 means none.
     const float* prev_rdm;

@@ -1401,7 +1401,7 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
     T.flag = a.flag ? a.flag + cpi * plane : nullptr;
     T.hits = a.hits ? a.hits + (size_t)wg * (C::W * P) : nullptr;
     T.hit_count = a.hit_count ? a.hit_count + wg : nullptr;
-    T.cell_base = (uint32_t)(cpi * plane);
+    T.cell_base = (uint32_t)(cpi * plane) + a.cell_off;
     T.bx = bx;
     if constexpr (C::W < 32) {   // 8 consecutive tiles on one XCD (workgroup x goes to XCD x % 8):
         // their partial RDM / flag row segments (W = 16: 64-B RDM and 16-B flag segments) meet
@@ -1532,7 +1532,7 @@ __global__ __launch_bounds__(MtdCfg<NF>::T) void mtd_bluestein_kernel(const floa
     const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
     o.hits = a.hits ? a.hits + (size_t)wg * ((size_t)W * P) : nullptr;
     o.lds_count = &s_hits;
-    o.cell0 = (uint32_t)cpi * plane + (uint32_t)v0 * R + (uint32_t)r;
+    o.cell0 = (uint32_t)cpi * plane + a.cell_off + (uint32_t)v0 * R + (uint32_t)r;
     float* sums = reinterpret_cast<float*>(smem) + W * C::MS + c * C::SMS + C::SPAD;
     doppler_sums(mag, sums, P, a.cv.ref, v0, v1);
     __syncthreads();
