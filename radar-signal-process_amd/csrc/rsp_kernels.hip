@@ -2366,32 +2366,44 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits_kernel(const float* __r
     cfar_hit_region<REF, SAVE>(rdm, flag, hits, counts, (int)blockIdx.x, region, a, (int)threadIdx.x, kHitThreads);
 }
 
-// The reference's window (5 reference + 7 guard cells): one wave per hit region, four regions
-// per workgroup.  A region is one MTD tile's hit list (~10-50 hits at c3-c5), so a workgroup
-// per region left most of its threads idle and took one dependent round-trip chain (count ->
-// index -> cells) per region; here the count and the lane's first index load together (the
-// index is in bounds past the count: a region holds W*P >= 256 entries), the lane's 17 cells
-// follow as one batch of range-checked buffer loads (RangeJob57's gathers), and hits past the
-// first 64 of a region follow in further batches of 64 the same way.
+// The reference's window (5 reference + 7 guard cells): LPR lanes per hit region (LPR = 64: one
+// wave per region, four regions per workgroup).  A region is one MTD tile's hit list (~10-50 hits
+// at c3-c5), so a workgroup per region left most of its threads idle and took one dependent
+// round-trip chain (count -> index -> cells) per region; here the count and the lane's first index
+// load together (the index is in bounds past the count: a region holds W*P >= 256 entries), the
+// lane's 17 cells follow as one batch of range-checked buffer loads (RangeJob57's gathers), and
+// hits past the first LPR of a region follow in further batches the same way (the batch loop runs
+// while any region of the wave has hits left, so every lane of the wave issues the gathers).
+template <int LPR>
 __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* __restrict__ rdm,
                                                                   uint8_t* __restrict__ flag,
                                                                   const uint32_t* __restrict__ hits,
                                                                   const uint32_t* __restrict__ counts, int nregions,
                                                                   int region, CfarRArgs a) {
-    const int rg = (int)(blockIdx.x * (kHitThreads / 64) + threadIdx.x / 64);
-    if (rg >= nregions) return;   // (wave-uniform; no barriers below)
-    const int k = (int)(threadIdx.x % 64);
+    constexpr int RPW = 64 / LPR;   // regions per wave
+    const int lane = (int)(threadIdx.x % 64);
+    const int rg = (int)((blockIdx.x * (kHitThreads / 64) + threadIdx.x / 64) * RPW) + lane / LPR;
+    if constexpr (RPW == 1) {
+        if (rg >= nregions) return;   // (wave-uniform; no barriers below)
+    }
+    const int k = lane % LPR;
     constexpr int NX = RangeJob57::NX;
-    const uint32_t* list = hits + (size_t)rg * region;
-    const uint32_t n = counts[rg];
+    const bool live = rg < nregions;
+    const uint32_t* list = hits + (size_t)(live ? rg : 0) * region;
+    const uint32_t n = live ? counts[rg] : 0u;
     uint32_t idx = list[k];
     const uint32_t R = (uint32_t)a.R, V = (uint32_t)a.V;
     const auto rr = buf_rsrc(rdm, kOob);
-    // batches of 64 hits, one per lane; the next batch's index is loaded before this batch's
-    // cells, so its round trip overlaps the gathers
-    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+    // batches of LPR hits per region, one per lane; the next batch's index is loaded before this
+    // batch's cells, so its round trip overlaps the gathers
+    for (uint32_t b0 = 0;; b0 += LPR) {
+        if constexpr (RPW == 1) {
+            if (b0 >= n) break;
+        } else {
+            if (__ballot(b0 < n) == 0) break;
+        }
         const bool mine = b0 + (uint32_t)k < n;
-        const uint32_t nk = b0 + 64u + (uint32_t)k;
+        const uint32_t nk = b0 + (uint32_t)LPR + (uint32_t)k;
         const uint32_t next = nk < n ? list[nk] : 0u;
         const uint32_t row = idx / R;
         const int r = (int)(idx - row * R);
@@ -2420,9 +2432,20 @@ hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hit
     // regions of P = 512 (c5: ~460 hits) keep a workgroup each (a wave took 12 -> 22 us).
     if (a.ref == 5 && a.save == 7 && region >= 64 && region <= 4096 &&
         (uint64_t)nregions * (uint64_t)region < (uint64_t)(kOob / 4u)) {
-        constexpr int RPB = kHitThreads / 64;
-        hipLaunchKernelGGL(cfar_hits57_kernel, dim3((unsigned)((nregions + RPB - 1) / RPB)), dim3(kHitThreads), 0, s,
-                           rdm, flag, hits, counts, nregions, region, a);
+        // lanes per region: 16 for the sparse hit lists of tiles of <= 128 Doppler rows (c3: ~11
+        // hits per region, range stage 37.5 -> 29.2 us per 16-chunk group, c3 +1.3 %), a wave for
+        // longer tiles (c4: ~50 hits, 46.6 us at 64 lanes against 50.1 at 32 and 56.0 at 16;
+        // profiles/r05/ab/range_stage_grouping.txt).  Dev A/B: environment RSP_HITS_LPR.
+        static const int lpr_env = [] { const char* v = getenv("RSP_HITS_LPR"); return v && *v ? atoi(v) : 0; }();
+        const int lpr = lpr_env > 0 ? lpr_env : (a.V <= 128 ? 16 : 64);
+        auto go = [&](auto kern, int rpw) {
+            const int rpb = (kHitThreads / 64) * rpw;   // regions per workgroup
+            hipLaunchKernelGGL(kern, dim3((unsigned)((nregions + rpb - 1) / rpb)), dim3(kHitThreads), 0, s, rdm, flag,
+                               hits, counts, nregions, region, a);
+        };
+        if (lpr == 16) go(cfar_hits57_kernel<16>, 4);
+        else if (lpr == 32) go(cfar_hits57_kernel<32>, 2);
+        else go(cfar_hits57_kernel<64>, 1);
     } else if (a.ref == 5 && a.save == 7)   // the reference's parameters
         hipLaunchKernelGGL((cfar_hits_kernel<5, 7>), dim3((unsigned)nregions), dim3(kHitThreads), 0, s, rdm, flag,
                            hits, counts, nregions, region, a);
