@@ -1146,6 +1146,15 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     // of a CPI belongs to one MTD thread), and the range stage, stream-ordered after that
     // chunk's MTD launch, writes the 1s: no separate fill pass
     m.flag_zero = 1;
+    // ... except for big chunks of long tiles: there a memset of the chunk's flag plane on the
+    // lane before its MTD (a streaming fill) beats the tiles' 16-byte row-segment stores (tiles of
+    // P >= 256 are 16 bins wide).  c4 (one 268 MB chunk per step): MTD 649 -> 572 us, +4.3 %;
+    // c3 (32-bin tiles, 8 MiB chunks) -2.8 %, c5 (8 MiB chunks) neutral
+    // (profiles/r05/ab/flag_memset.txt).  Dev A/B: RSP_FLAG_MEMSET 0 / 1 forces it off / on.
+    static const int fenv = [] { const char* v = getenv("RSP_FLAG_MEMSET"); return v && *v ? atoi(v) : -1; }();
+    const bool fm = cfar && cr.rflag && d_flag &&
+                    (fenv >= 0 ? fenv == 1 : (V >= 256 && (uint64_t)cells >= (64ull << 20)));
+    if (fm) m.flag_zero = 0;
     // Chunk k runs on lane k % ns (lane 0 = the caller's stream), each lane with its own
     // scratch slot, so PC of one chunk overlaps MTD / CFAR of the previous one.  The lanes
     // fork from and join back into the caller's stream.
@@ -1209,6 +1218,7 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
                 m.prev_cr = cr;
             }
         }
+        if (fm) HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ls));
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
             Pending& pv = pend[lane];
