@@ -2380,13 +2380,16 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* _
                                                                   const uint32_t* __restrict__ hits,
                                                                   const uint32_t* __restrict__ counts, int nregions,
                                                                   int region, CfarRArgs a) {
-    constexpr int RPW = 64 / LPR;   // regions per wave
+    // LPR <= 64: 64 / LPR regions per wave; LPR > 64 (a multiple of 64): a region spans LPR / 64
+    // waves (the dense lists of 8192-cell regions, c5)
+    constexpr int RPW = LPR >= 64 ? 1 : 64 / LPR;
     const int lane = (int)(threadIdx.x % 64);
-    const int rg = (int)((blockIdx.x * (kHitThreads / 64) + threadIdx.x / 64) * RPW) + lane / LPR;
+    const int rg = LPR > 64 ? (int)(blockIdx.x * (kHitThreads / LPR) + threadIdx.x / LPR)
+                            : (int)((blockIdx.x * (kHitThreads / 64) + threadIdx.x / 64) * RPW) + lane / LPR;
     if constexpr (RPW == 1) {
         if (rg >= nregions) return;   // (wave-uniform; no barriers below)
     }
-    const int k = lane % LPR;
+    const int k = LPR > 64 ? (int)(threadIdx.x % LPR) : lane % LPR;
     constexpr int NX = RangeJob57::NX;
     const bool live = rg < nregions;
     const uint32_t* list = hits + (size_t)(live ? rg : 0) * region;
@@ -2423,6 +2426,15 @@ __global__ __launch_bounds__(kHitThreads) void cfar_hits57_kernel(const float* _
     }
 }
 
+// Regions larger than 4096 cells (P = 512 tiles: c5's ~460 hits per region) take a workgroup
+// each with the batched, branch-free gathers of cfar_hits57_kernel: c5 range stage 64 -> 50 us per
+// 16-CPI group, +0.9 % (profiles/r05/ab/range_stage_grouping.txt).  Dev A/B: RSP_HITS_BIG=0
+// restores the per-hit loads of cfar_hits_kernel.
+static bool hits_big() {
+    static const bool b = [] { const char* v = getenv("RSP_HITS_BIG"); return !(v && *v == '0'); }();
+    return b;
+}
+
 hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hits, const uint32_t* counts,
                             int nregions, int region, const CfarRArgs& a, hipStream_t s) {
     if (nregions <= 0) return hipSuccess;
@@ -2446,6 +2458,11 @@ hipError_t launch_cfar_hits(const float* rdm, uint8_t* flag, const uint32_t* hit
         if (lpr == 16) go(cfar_hits57_kernel<16>, 4);
         else if (lpr == 32) go(cfar_hits57_kernel<32>, 2);
         else go(cfar_hits57_kernel<64>, 1);
+    } else if (a.ref == 5 && a.save == 7 && region >= kHitThreads && hits_big() &&
+               (uint64_t)nregions * (uint64_t)region < (uint64_t)(kOob / 4u)) {
+        // larger regions: the batched gathers with the whole workgroup on a region
+        hipLaunchKernelGGL(cfar_hits57_kernel<kHitThreads>, dim3((unsigned)nregions), dim3(kHitThreads), 0, s, rdm, flag,
+                           hits, counts, nregions, region, a);
     } else if (a.ref == 5 && a.save == 7)   // the reference's parameters
         hipLaunchKernelGGL((cfar_hits_kernel<5, 7>), dim3((unsigned)nregions), dim3(kHitThreads), 0, s, rdm, flag,
                            hits, counts, nregions, region, a);
