@@ -365,3 +365,32 @@ def test_chain_cfar_tile_mappings(torch_cuda, P, R):
     assert hard == 0, (hard, soft)
     assert soft <= max(2, flag.size // 100000), soft
     assert flag.sum() > 0
+
+
+def test_range_groups_across_group_boundaries(torch_cuda):
+    """The grouped range stage (rsp_capi.cpp run_chain_body: the range CFAR of up to 16 chunks of a
+    pipeline in one launch, hit indices relative to the group's first output cell): 37 one-CPI
+    chunks on two pipelines (groups of 16 + a partial group each), 8 chunks of 5 with a short last
+    chunk, and one 37-CPI chunk give the same RDM and flags, bit for bit."""
+    torch = torch_cuda
+    from rsp import presets, synth
+    from rsp.engine import Engine
+    spec = presets.v2(64, 1024)
+    cf = presets.default_cfar(spec)
+    B = 37
+    echo = synth.echo_numpy(spec, B, seed=3737)
+    d_in = torch.from_numpy(echo).cuda()
+    V, Ro = spec.V, spec.R_out
+    outs = []
+    for chunk in (1, 5, 37):
+        eng = Engine(spec, chunk=chunk)
+        r = torch.empty((B, V, Ro), dtype=torch.float32, device="cuda")
+        f = torch.empty((B, V, Ro), dtype=torch.uint8, device="cuda")
+        eng.run_dev(d_in, rdm=r, flag=f, cfar=cf)
+        torch.cuda.synchronize()
+        outs.append((r.cpu().numpy(), f.cpu().numpy()))
+        eng.close()
+    assert outs[0][1].sum() > 0
+    for r, f in outs[1:]:
+        np.testing.assert_array_equal(r, outs[0][0])
+        np.testing.assert_array_equal(f, outs[0][1])
