@@ -73,9 +73,6 @@ def parse():
     ap.add_argument("--prefilter", action="store_true",
                     help="fused iSTC (a synthetic stc curve) + MTI lag 30 in the chain (rsp_set_prefilter)")
     ap.add_argument("--streams", type=int, default=0, help="chunk pipelines (0 = library default)")
-    ap.add_argument("--flow", type=int, default=None,
-                    help="rsp_set_flow schedule: 0 chunked pipelines, 1/2 one persistent dataflow launch "
-                         "(default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--profile-every", type=int, default=7,
@@ -786,8 +783,6 @@ def main():
     spec = presets.make(args.preset, args.P, args.R)
     cfar = None if args.no_cfar else presets.default_cfar(spec)
     eng = Engine(spec, device=local, chunk=args.chunk, streams=args.streams)
-    if args.flow is not None:
-        eng.set_flow(args.flow)
     if args.prefilter:
         import numpy as np
         from rsp.prefilter import istc_gain
@@ -916,10 +911,19 @@ def main():
                 avg_us = ms * 1e3 / max(n, 1)
                 k = {"avg_us": round(avg_us, 2), "launches_per_step": n, "ms_per_step": round(ms, 3)}
                 if name in per_kernel_bytes:
+                    # `frac`: the kernel's own compulsory I/O (PC: echo in + scratch out; MTD:
+                    # scratch in + RDM / flags out) per launch / its time / peak
                     ab = per_kernel_bytes[name]
-                    k["alg_bytes_per_launch"] = int(ab)
+                    k["io_bytes_per_launch"] = int(ab)
                     k["achieved"] = round(ab / (avg_us * 1e3), 1)
                     k["frac"] = round(ab / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
+                    k["frac_basis"] = "own I/O (incl. the PC->MTD scratch)"
+                # `frac_alg` (the contract's definition): the chain's algorithmic bytes
+                # per unit x the units one launch processes / the launch's average time / peak
+                upl = units / max(n, 1)
+                k["units_per_launch"] = round(upl, 3)
+                k["alg_bytes_per_launch"] = int(upl * cpi_bytes)
+                k["frac_alg"] = round(upl * cpi_bytes / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
                 if pmc and name in pmc.get("kernels", {}):
                     pk = pmc["kernels"][name]
                     k["hbm_bytes_per_launch"] = pk.get("hbm_bytes_per_launch")
@@ -936,6 +940,7 @@ def main():
             dom = max(kernels, key=lambda q: kernels[q][0])
             roof["dominant_kernel"] = dom
             roof["dominant_ms_per_step"] = round(kernels[dom][0], 3)
+            roof["dominant_frac_alg"] = ks[dom]["frac_alg"]
             if "valu_frac" in ks.get(dom, {}):
                 roof["valu_frac"] = ks[dom]["valu_frac"]
                 roof["valu_frac_source"] = "profiles/pmc_%s.json (dominant kernel, SQ counters)" % tag

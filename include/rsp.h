@@ -49,8 +49,12 @@
 extern "C" {
 #endif
 
-#define RSP_ABI_VERSION 3   /* 2: rsp_set_fused / rsp_chain_check removed, rsp_set_pc_split added;
-                               3: rsp_set_host_pipeline */
+#define RSP_ABI_VERSION 4   /* 2: rsp_set_fused / rsp_chain_check removed, rsp_set_pc_split added;
+                               3: rsp_set_host_pipeline;
+                               4: rsp_set_flow / rsp_flow_status (round 5's opt-in dataflow launch,
+                                  with its RSP_K_FLOW profile slot) removed; rsp_profile_read_n
+                                  takes the arrays' length, rsp_profile_read writes exactly the 4
+                                  ABI-3 entries */
 #define RSP_MAX_SEG 4
 #define RSP_MAX_FIR_TAPS 64
 
@@ -403,34 +407,19 @@ int rsp_prefilter_dev(rsp_ctx* ctx, const void* d_in, void* d_out, int64_t P, in
  * stage: its rows are PC(gain .* x). */
 int rsp_set_prefilter(rsp_ctx* ctx, const float* gain /* nullable, host [R] */, int32_t mti_lag);
 
-/* Schedule of the device chain (rsp_pc_mtd_cfar_dev and the host-buffer calls above it).
- * mode 0 (default): chunks of CPIs through two stream pipelines, one PC and one MTD launch per
- * chunk, the PC rows handed over through a scratch buffer (the corner turn between
- * fun_lss_pulse_compression.m:36-65 and fun_Process_MTD.m:27-37).  mode 1 / 2: the whole call
- * as ONE persistent launch -- PC rows, MTD tiles and range-CFAR jobs are work items of per-XCD
- * queues, the corner turn goes through a ring of 3 scratch CPIs per queue, and each hand-off is
- * a counter in memory instead of a kernel boundary (1: a CPI's MTD tiles queued after the next
- * CPI's PC rows; 2: the two interleaved).  Outputs are bit-identical to mode 0.  The dataflow is
- * built for the v2 c2/c3 shape (128 pulses, 1024 + 4096-point matched filters, one beam, CFAR
- * with the reference's 5 + 7 windows or none, no fused pre-filter); other contexts and calls
- * keep mode 0 whatever is set. */
-int rsp_set_flow(rsp_ctx* ctx, int32_t mode);   /* (mode + 4 * lead + 16 * lag: dev tuning bits, see rsp_capi.cpp) */
-/* After a dataflow call: *timed_out = 1 if a hand-off wait of the last launch exceeded its
- * bound (0.5 s) -- the launch then finished with unspecified outputs instead of hanging.
- * Synchronises the device. */
-int rsp_flow_status(rsp_ctx* ctx, int32_t* timed_out);
-
 /* ---- diagnostics ---------------------------------------------------------------------- */
 /* Per-kernel device time accumulated from HIP events recorded on the launch stream around
  * kernel launches while profiling is enabled: enable = 1 brackets every launch, enable = N > 1
  * every N-th launch (sampling: each event pair costs the stream a few microseconds),
  * 0 stops.  Any call resets the counters.
- * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V, RSP_K_FLOW (the one-launch
- * dataflow of rsp_set_flow). */
-#define RSP_NKERNELS 5
-enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3, RSP_K_FLOW = 4 };
+ * Kernel ids: RSP_K_PC, RSP_K_MTD, RSP_K_CFAR_R, RSP_K_CFAR_V. */
+#define RSP_NKERNELS 4
+enum { RSP_K_PC = 0, RSP_K_MTD = 1, RSP_K_CFAR_R = 2, RSP_K_CFAR_V = 3 };
 int rsp_profile(rsp_ctx* ctx, int32_t enable);
-/* Waits for the recorded events; ms[k] = summed device time, launches[k] = launch count. */
+/* Waits for the recorded events; ms[k] = summed device time, launches[k] = launch count, for
+ * k < n (n <= RSP_NKERNELS entries are written; pass the length of both arrays). */
+int rsp_profile_read_n(rsp_ctx* ctx, double* ms, int64_t* launches, int32_t n);
+/* ABI-3 form: writes exactly 4 entries (RSP_K_PC .. RSP_K_CFAR_V), whatever RSP_NKERNELS is. */
 int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches);
 
 #ifdef __cplusplus

@@ -59,7 +59,14 @@ struct rsp_ctx {
     int64_t chunk = 0;  // 0 = default
     int nstreams = 0;   // chunk pipelines (the caller's stream + nstreams-1 internal ones); 0 = default
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+    // (dev A/B, RSP_CU_SPLIT) PC and MTD on two CU-masked streams, chunk k's slot k % kSplitSlots
+    static constexpr int kSplitSlots = 3;
+    hipStream_t cm_pc = nullptr, cm_mtd = nullptr;
+    hipEvent_t ev_pd[kSplitSlots] = {}, ev_md[kSplitSlots] = {}, ev_sj = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+    // flag-plane memset of big window chunks on a side stream, beside the chunk's PC
+    hipStream_t s_fm = nullptr;
+    hipEvent_t ev_fm0 = nullptr, ev_fm1 = nullptr;
     // The context's scratch (PC corner turn, hit lists, internal RDM, flagV staging) is reused by
     // every _dev call: a call's stream waits for the previous call's release event first, so
     // calls on different streams never overlap on it.
@@ -71,10 +78,6 @@ struct rsp_ctx {
     DevBuf pf_gain;                     // fused iSTC gains (rsp_set_prefilter)
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
-    // persistent dataflow (rsp_set_flow): scratch ring, hit-list ring, counts, control words,
-    // RDM ring (when the caller takes no RDM)
-    int flow = 0;
-    DevBuf fl_ring, fl_hring, fl_hcount, fl_ctl, fl_rdm;
     DevBuf meas_band;                   // measurement: per-(CPI, band, column) hit counts
     DevBuf ing_meta;                    // ingest: per-PRT record offsets and types
     DevBuf st_in, st_canon, st_rdm, st_flag, st_flagV, st_t;  // host-API staging (rsp_cfar)
@@ -94,6 +97,8 @@ struct rsp_ctx {
         int ring_in = 0;                      // next input piece slot
         int threads = 0;                      // requested copy threads (0 = default)
         std::unique_ptr<rsp::CopyPool> pool;
+        std::unique_ptr<rsp::Prefaulter> prefault;   // fresh output arrays (host_prefault)
+        rsp::Prefaulter* pf = nullptr;                // the running call's prefault job, if any
         // one-chunk calls (host_chain_small): pinned staging the kernels read and write directly
         static constexpr int kParts = 16;     // output parts in flight (one event each)
         void* zc_in = nullptr;
@@ -296,7 +301,7 @@ static void zero_v_band(int64_t rows, int div, int* lo, int* hi) {
 }
 
 // ------------------------------------------------------------------ public API
-const char* rsp_version(void) { return "rsp-mi355x 0.4.0 (gfx950, abi 3)"; }
+const char* rsp_version(void) { return "rsp-mi355x 0.5.0 (gfx950, abi 4)"; }
 
 const char* rsp_last_error(const rsp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
@@ -306,8 +311,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
-                      &ctx->meas_band, &ctx->ing_meta, &ctx->fl_ring, &ctx->fl_hring, &ctx->fl_hcount,
-                      &ctx->fl_ctl, &ctx->fl_rdm};
+                      &ctx->meas_band, &ctx->ing_meta};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -316,6 +320,13 @@ int rsp_destroy(rsp_ctx* ctx) {
     }
     for (int i = 0; i < 3; ++i) {
         if (ctx->aux[i]) hipStreamDestroy(ctx->aux[i]);
+    if (ctx->cm_pc) hipStreamDestroy(ctx->cm_pc);
+    if (ctx->cm_mtd) hipStreamDestroy(ctx->cm_mtd);
+    for (int i = 0; i < rsp_ctx::kSplitSlots; ++i) {
+        if (ctx->ev_pd[i]) hipEventDestroy(ctx->ev_pd[i]);
+        if (ctx->ev_md[i]) hipEventDestroy(ctx->ev_md[i]);
+    }
+    if (ctx->ev_sj) hipEventDestroy(ctx->ev_sj);
         if (ctx->ev_join[i]) hipEventDestroy(ctx->ev_join[i]);
     }
     {
@@ -344,6 +355,9 @@ int rsp_destroy(rsp_ctx* ctx) {
         h.pool.reset();
     }
     if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
+    if (ctx->s_fm) hipStreamDestroy(ctx->s_fm);
+    if (ctx->ev_fm0) hipEventDestroy(ctx->ev_fm0);
+    if (ctx->ev_fm1) hipEventDestroy(ctx->ev_fm1);
     if (ctx->ev_scratch) hipEventDestroy(ctx->ev_scratch);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -510,7 +524,6 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
             if (pc.seg[s].kind != RSP_SEG_MF) continue;
             rsp::PcMfArgs a;
             std::memset(&a, 0, sizeof(a));
-            a.cpi_rows = (int)p.P;
             a.R = (int)p.R;
             a.R_out = (int)p.R_out;
             a.mf = pc.seg[s];
@@ -736,30 +749,6 @@ int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis) {
 
 static bool set_device(rsp_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess; }
 
-int rsp_set_flow(rsp_ctx* ctx, int32_t mode) {
-    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_flow: null ctx");
-    // mode bits: 0-1 order (0 off, 1 blocked, 2 interleaved); 2-3 PC lead, 4-5 range-job lag (0 = the
-    // default 2; 1 or 2): tuning for A/B runs
-    const int order = mode & 3, lead = (mode >> 2) & 3, lag = (mode >> 4) & 3;
-    if (mode < 0 || mode > 63 || order == 3 || lead == 3 || lag == 3 || (order == 0 && mode != 0))
-        return fail(ctx, RSP_ERR_ARG, "rsp_set_flow: bad mode %d", mode);
-    ctx->flow = mode;
-    return RSP_OK;
-}
-
-int rsp_flow_status(rsp_ctx* ctx, int32_t* timed_out) {
-    if (!ctx || !timed_out) return fail(ctx, RSP_ERR_ARG, "rsp_flow_status: null argument");
-    *timed_out = 0;
-    if (!ctx->fl_ctl.p) return RSP_OK;
-    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
-    uint32_t w = 0;
-    HIP_TRY(ctx, hipDeviceSynchronize());
-    HIP_TRY(ctx, hipMemcpy(&w, (const char*)ctx->fl_ctl.p + (size_t)(rsp::kFlowCtlLines - 1) * rsp::kFlowLine * 4, 4,
-                           hipMemcpyDeviceToHost));
-    *timed_out = (int32_t)w;
-    return RSP_OK;
-}
-
 static int64_t chunk_of(const rsp_ctx* ctx, int64_t batch) {
     int64_t c = ctx->chunk;
     if (c <= 0) {
@@ -914,8 +903,8 @@ int rsp_profile(rsp_ctx* ctx, int32_t enable) {
     return RSP_OK;
 }
 
-int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches) {
-    if (!ctx || !ms || !launches) return fail(ctx, RSP_ERR_ARG, "rsp_profile_read: null argument");
+int rsp_profile_read_n(rsp_ctx* ctx, double* ms, int64_t* launches, int32_t n) {
+    if (!ctx || !ms || !launches || n < 0) return fail(ctx, RSP_ERR_ARG, "rsp_profile_read_n: bad argument");
     for (size_t i = 0; i < ctx->nev; ++i) {
         rsp_ctx::Ev& e = ctx->evs[i];
         HIP_TRY(ctx, hipEventSynchronize(e.b));
@@ -925,11 +914,17 @@ int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches) {
         ctx->prof_n[e.k] += 1;
     }
     ctx->nev = 0;
-    for (int k = 0; k < RSP_NKERNELS; ++k) {
+    for (int k = 0; k < n && k < RSP_NKERNELS; ++k) {
         ms[k] = ctx->prof_ms[k];
         launches[k] = ctx->prof_n[k];
     }
     return RSP_OK;
+}
+
+// the ABI-3 form: exactly the four kernel ids that header declared (RSP_K_PC .. RSP_K_CFAR_V)
+int rsp_profile_read(rsp_ctx* ctx, double* ms, int64_t* launches) {
+    if (!ctx || !ms || !launches) return fail(ctx, RSP_ERR_ARG, "rsp_profile_read: null argument");
+    return rsp_profile_read_n(ctx, ms, launches, 4);
 }
 
 int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, void* d_pc, void* stream) {
@@ -976,65 +971,6 @@ int rsp_set_prefilter(rsp_ctx* ctx, const float* gain, int32_t mti_lag) {
     return RSP_OK;
 }
 
-// The whole call as one persistent dataflow launch (rsp_set_flow; FlowArgs in rsp_internal.h).
-// RSP_ERR_UNSUPPORTED (without touching the error text) when the context or call is outside what
-// the dataflow kernel is built for -- the caller then runs the chunked pipeline.
-static int run_flow(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncpi, const rsp::MtdArgs& m,
-                    const rsp::CfarRArgs& cr, bool cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                    hipStream_t s) {
-    const int64_t P = ctx->p.P, Ro = ctx->p.R_out;
-    if (!ctx->pc_v2 || ctx->pc_mf.size() != 2 || ctx->beams != 1 || ctx->V != P || m.pin != P || m.bnf > 0 ||
-        m.mti_lag > 0 || ctx->pc_mf[0].gain || ctx->pc_mf[1].gain ||
-        !rsp::flow_supported((int)P, ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft, dtype, ctx->beams))
-        return RSP_ERR_UNSUPPORTED;
-    if (cfar && !(m.cv.ref == 5 && m.cv.save == 7 && (!cr.rflag || (cr.ref == 5 && cr.save == 7))))
-        return RSP_ERR_UNSUPPORTED;
-    if (ncpi > 0x7fffffff / 2) return RSP_ERR_UNSUPPORTED;
-    int nreg = 0, reg = 0;
-    rsp::mtd_regions((int)P, (int)Ro, 1, &nreg, &reg, 1);   // per CPI: tiles, entries per tile
-    constexpr int64_t Q = rsp::kFlowQueues, S = rsp::kFlowSlots;
-    const int64_t Qn = ncpi < Q ? ncpi : Q;                 // queues in use
-    const size_t plane = (size_t)P * Ro;
-    int rc;
-    if ((rc = ensure(ctx, ctx->fl_ring, (size_t)Qn * S * plane * sizeof(float2)))) return rc;
-    if ((rc = ensure(ctx, ctx->fl_ctl, (size_t)rsp::kFlowCtlLines * rsp::kFlowLine * sizeof(uint32_t)))) return rc;
-    const bool hits = cfar && cr.rflag;
-    if (hits) {
-        if ((rc = ensure(ctx, ctx->fl_hring, (size_t)Qn * S * nreg * reg * sizeof(uint32_t)))) return rc;
-        if ((rc = ensure(ctx, ctx->fl_hcount, (size_t)Qn * S * nreg * sizeof(uint32_t)))) return rc;
-    }
-    if (!d_rdm && (rc = ensure(ctx, ctx->fl_rdm, (size_t)Qn * S * plane * sizeof(float)))) return rc;
-    rsp::FlowArgs f;
-    std::memset(&f, 0, sizeof(f));
-    f.echo = d_echo;
-    f.a1 = ctx->pc_mf[0];
-    f.a2 = ctx->pc_mf[1];
-    f.a1.rows = f.a2.rows = (int)P;
-    f.m = m;
-    f.m.flag_zero = 1;
-    f.m.rflag = cr.rflag;
-    f.m.flag = nullptr;
-    f.m.hits = nullptr;
-    f.m.hit_count = nullptr;
-    f.m.prev_nregions = 0;
-    f.cr = cr;
-    f.ring = (float2*)ctx->fl_ring.p;
-    f.hring = hits ? (uint32_t*)ctx->fl_hring.p : nullptr;
-    f.hcount = hits ? (uint32_t*)ctx->fl_hcount.p : nullptr;
-    f.rdm_ring = d_rdm ? 0 : 1;
-    f.rdm = d_rdm ? d_rdm : (float*)ctx->fl_rdm.p;
-    f.flag = cfar ? d_flag : nullptr;
-    f.flagV = cfar ? d_flagV : nullptr;
-    f.ctl = (uint32_t*)ctx->fl_ctl.p;
-    f.ncpi = (int)ncpi;
-    f.order = ctx->flow & 3;
-    f.lead = (ctx->flow >> 2) & 3 ? (ctx->flow >> 2) & 3 : 2;
-    f.lag = (ctx->flow >> 4) & 3 ? (ctx->flow >> 4) & 3 : 2;
-    HIP_TRY(ctx, hipMemsetAsync(ctx->fl_ctl.p, 0, ctx->fl_ctl.n, s));
-    HIP_TRY(ctx, timed(ctx, RSP_K_FLOW, s, [&] { return rsp::launch_flow(f, dtype, s); }));
-    return RSP_OK;
-}
-
 // The chain over `units` on stream s.  win == 0: a unit is one CPI ([P][R] input rows).
 // win > 0: a unit is a frame pair (n, n+1) of a frame-contiguous input holding units + 1
 // frames, producing `win` windowed CPIs (MtdArgs::win); a chunk computes the PC of its
@@ -1061,6 +997,32 @@ static int range_group() {
     return g;
 }
 
+// (dev A/B of VERDICT r5 item 1) RSP_CU_SPLIT=n: PC launches on a stream whose CU mask holds bits
+// [0, 8n) -- the mask bits spread over the XCDs (tools/micro/cumask_probe.hip) -- and the MTD and
+// range launches on a stream with the other bits, chained by events through kSplitSlots scratch
+// slots (PC(k) waits for MTD(k - slots); MTD(k) waits for PC(k)).  Not the product schedule.
+static int cu_split() {
+    static const int n = [] { const char* v = getenv("RSP_CU_SPLIT"); return v && *v ? atoi(v) : 0; }();
+    return n;
+}
+static int split_streams(rsp_ctx* ctx) {
+    if (ctx->cm_pc) return RSP_OK;
+    int ncu = 0;
+    HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int words = (ncu + 31) / 32, npc = 8 * cu_split();
+    if (npc <= 0 || npc >= ncu) return fail(ctx, RSP_ERR_ARG, "RSP_CU_SPLIT=%d: %d of %d CUs", cu_split(), npc, ncu);
+    std::vector<uint32_t> mp((size_t)words, 0u), mm((size_t)words, 0u);
+    for (int b = 0; b < ncu; ++b) (b < npc ? mp : mm)[(size_t)(b / 32)] |= 1u << (b % 32);
+    HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->cm_pc, (uint32_t)words, mp.data()));
+    HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->cm_mtd, (uint32_t)words, mm.data()));
+    for (int i = 0; i < rsp_ctx::kSplitSlots; ++i) {
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_pd[i], hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_md[i], hipEventDisableTiming));
+    }
+    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_sj, hipEventDisableTiming));
+    return RSP_OK;
+}
+
 static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
                           const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
                           float* d_diff, hipStream_t s, bool pc_input) {
@@ -1073,10 +1035,6 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         if (rc) return rc;
     } else {
         m.cv.enabled = 0;
-    }
-    if (ctx->flow > 0 && win == 0 && !pc_input && !d_diff) {
-        const int rc = run_flow(ctx, d_echo, dtype, units, m, cr, cfar != nullptr, d_rdm, d_flag, d_flagV, s);
-        if (rc != RSP_ERR_UNSUPPORTED) return rc;   // (not this shape: the chunked pipeline below)
     }
     const int64_t ocpi = win > 0 ? win : 1;               // output CPIs per unit
     m.nwin = win;
@@ -1104,12 +1062,15 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     std::vector<int64_t> cstart{0};
     while (cstart.back() < units) cstart.push_back(cstart.back() + cu < units ? cstart.back() + cu : units);
     const int64_t nchunks = (int64_t)cstart.size() - 1;
-    const int ns = (int)(nsd < nchunks ? nsd : nchunks);
+    const bool split = cu_split() > 0 && win == 0 && !pc_input;
+    const int ns = split ? 1 : (int)(nsd < nchunks ? nsd : nchunks);
+    const int pslots = split ? rsp_ctx::kSplitSlots : ns;   // PC scratch slots
     const size_t plane = (size_t)V * Ro;                  // output cells per CPI
     const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
     const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * NB * P;
-    int rc = pc_input ? RSP_OK : ensure(ctx, ctx->scratch_pc, (size_t)ns * pcrows * Ro * sizeof(float2));
+    int rc = pc_input ? RSP_OK : ensure(ctx, ctx->scratch_pc, (size_t)pslots * pcrows * Ro * sizeof(float2));
     if (rc) return rc;
+    if (split && (rc = split_streams(ctx))) return rc;
     int nreg = 0, reg = 0;
     if (cfar) {
         // fused range stage: per-lane hit lists, one region per MTD workgroup sized to its
@@ -1155,10 +1116,27 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     const bool fm = cfar && cr.rflag && d_flag &&
                     (fenv >= 0 ? fenv == 1 : (V >= 256 && (uint64_t)cells >= (64ull << 20)));
     if (fm) m.flag_zero = 0;
+    // ... on a side stream that forks from the lane before the chunk's PC and joins it before the
+    // MTD, so the fill runs beside the PC instead of between PC and MTD (c4's
+    // ~45 us memset per step).  Dev A/B: RSP_FLAG_MEMSET_SIDE=0 puts it back on the lane.
+    static const int fside = [] { const char* v = getenv("RSP_FLAG_MEMSET_SIDE"); return v && *v ? atoi(v) : 1; }();
+    const bool fms = fm && fside != 0 && !pc_input;
+    if (fms && !ctx->s_fm) {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->s_fm, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fm0, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fm1, hipEventDisableTiming));
+    }
     // Chunk k runs on lane k % ns (lane 0 = the caller's stream), each lane with its own
     // scratch slot, so PC of one chunk overlaps MTD / CFAR of the previous one.  The lanes
     // fork from and join back into the caller's stream.
     hipStream_t lanes[4] = {s, nullptr, nullptr, nullptr};
+    if (split) {   // fork both masked streams from the caller's; lane 0 = the MTD stream
+        if (!ctx->ev_fork) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->cm_pc, ctx->ev_fork, 0));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->cm_mtd, ctx->ev_fork, 0));
+        lanes[0] = ctx->cm_mtd;
+    }
     if (ns > 1) {
         if (!ctx->ev_fork) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
@@ -1196,8 +1174,23 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         if (pc_input) {   // d_echo already holds pulse-compressed rows [units][beams][P][R_out]
             pcs = (float2*)d_echo + (size_t)u0 * NB * P * Ro;
         } else {
-            pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
-            HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls));
+            if (fms) {   // the flag fill of this chunk beside its PC (the lane's earlier work is done with it)
+                HIP_TRY(ctx, hipEventRecord(ctx->ev_fm0, ls));
+                HIP_TRY(ctx, hipStreamWaitEvent(ctx->s_fm, ctx->ev_fm0, 0));
+                HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ctx->s_fm));
+                HIP_TRY(ctx, hipEventRecord(ctx->ev_fm1, ctx->s_fm));
+            }
+            if (split) {
+                const int sl = (int)(k % rsp_ctx::kSplitSlots);
+                pcs = (float2*)ctx->scratch_pc.p + sl * pcrows * Ro;
+                if (k >= rsp_ctx::kSplitSlots) HIP_TRY(ctx, hipStreamWaitEvent(ctx->cm_pc, ctx->ev_md[sl], 0));
+                HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * NB * P, ctx->cm_pc));
+                HIP_TRY(ctx, hipEventRecord(ctx->ev_pd[sl], ctx->cm_pc));
+                HIP_TRY(ctx, hipStreamWaitEvent(ls, ctx->ev_pd[sl], 0));
+            } else {
+                pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
+                HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls));
+            }
         }
         m.diff = d_diff ? d_diff + o0 : nullptr;
         m.prev_nregions = 0;
@@ -1218,7 +1211,8 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
                 m.prev_cr = cr;
             }
         }
-        if (fm) HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ls));
+        if (fms) HIP_TRY(ctx, hipStreamWaitEvent(ls, ctx->ev_fm1, 0));
+        else if (fm) HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ls));
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
             Pending& pv = pend[lane];
@@ -1245,6 +1239,7 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
                 pv.nreg = 0;
             }
         }
+        if (split) HIP_TRY(ctx, hipEventRecord(ctx->ev_md[(int)(k % rsp_ctx::kSplitSlots)], ls));
     }
     for (int lane = 0; lane < ns; ++lane) {   // each lane's last chunk
         const Pending& pv = pend[lane];
@@ -1256,6 +1251,10 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     for (int i = 1; i < ns; ++i) {
         HIP_TRY(ctx, hipEventRecord(ctx->ev_join[i - 1], lanes[i]));
         HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join[i - 1], 0));
+    }
+    if (split) {   // join: the MTD stream's last work follows every PC; the caller's stream waits for it
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_sj, ctx->cm_mtd));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_sj, 0));
     }
     return RSP_OK;
 }
@@ -1679,6 +1678,7 @@ static int d2h_pieces(rsp_ctx* ctx, const std::vector<D2HPart>& parts) {
     for (size_t i = 0; i < np; ++i) {
         const int r = (int)(i % h.kRing);
         HIP_TRY(ctx, hipEventSynchronize(h.ev_pin_out[r]));
+        if (h.pf) h.pf->wait(ps[i].h, ps[i].n * (ps[i].widen == 1 ? 2 : (ps[i].widen == 2 ? 8 : 1)));
         if (ps[i].widen == 1) pool.widen_f32((double*)ps[i].h, (const float*)h.pin_out[r], ps[i].n / 4);
         else if (ps[i].widen == 2) pool.widen_u8((double*)ps[i].h, (const uint8_t*)h.pin_out[r], ps[i].n);
         else pool.copy(ps[i].h, h.pin_out[r], ps[i].n);
@@ -1871,6 +1871,7 @@ static int zc_deliver(rsp_ctx* ctx, const ZcOut* outs, int nout, int64_t batch, 
         HIP_TRY(ctx, hipEventSynchronize(h.ev_part[q]));
         const double t1 = ht.now_us();
         const char* zp = zk[pt.k] + pt.off * o.es;
+        if (h.pf) h.pf->wait((char*)o.host + pt.off * (o.f64 ? 8 : o.es), pt.n * (o.f64 ? 8 : o.es));
         if (o.es == 4) {
             if (o.f64) pool.widen_f32((double*)o.host + pt.off, (const float*)zp, pt.n);
             else pool.copy((float*)o.host + pt.off, zp, pt.n * 4);
@@ -1963,6 +1964,40 @@ static int host_chain_small(rsp_ctx* ctx, const void* echo, int32_t dtype, int32
     return RSP_OK;
 }
 
+// Prefault of the caller's output arrays (rsp_hostpool.h Prefaulter) from the start of a call
+// whose outputs total >= kPrefaultMin bytes: new arrays of that size are fresh anonymous
+// mappings (glibc serves allocations above its mmap threshold, at most 32 MiB, by mmap), and
+// the copy threads would otherwise take one page fault + zeroing per 4 KiB as they deliver.
+// The job ends (workers off the caller's memory) before the call returns, on every path.
+// Dev A/B: RSP_PREFAULT=0 off; RSP_PREFAULT_THREADS (default 4); RSP_PREFAULT_HUGE=0 (no
+// MADV_HUGEPAGE advice).
+static constexpr size_t kPrefaultMin = 8u << 20;
+struct PrefaultJob {
+    rsp_ctx* ctx = nullptr;
+    ~PrefaultJob() {
+        if (ctx && ctx->hp.pf) {
+            ctx->hp.pf->end();
+            ctx->hp.pf = nullptr;
+        }
+    }
+};
+static void host_prefault(rsp_ctx* ctx, PrefaultJob& job, const std::vector<std::pair<void*, size_t>>& ranges) {
+    static const int mode = zc_knob("RSP_PREFAULT", 1);
+    static const int nthr = zc_knob("RSP_PREFAULT_THREADS", 4);
+    static const int huge = zc_knob("RSP_PREFAULT_HUGE", 1);
+    size_t total = 0;
+    for (const auto& r : ranges) total += r.first ? r.second : 0;
+    if (mode == 0 || total < kPrefaultMin) return;
+    auto& h = ctx->hp;
+    if (!h.prefault) h.prefault.reset(new rsp::Prefaulter(nthr, huge != 0));
+    std::vector<std::pair<void*, size_t>> rs;
+    for (const auto& r : ranges)
+        if (r.first && r.second) rs.push_back(r);
+    h.prefault->begin(rs);
+    h.pf = h.prefault.get();
+    job.ctx = ctx;
+}
+
 static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t layout, int64_t P, int64_t R,
                       int64_t batch, const rsp_cfar_params* cfar, void* rdm_out, int32_t out_layout,
                       void* flag_out, void* flagV_out, bool f64) {
@@ -1994,6 +2029,12 @@ static int host_chain(rsp_ctx* ctx, const void* echo, int32_t dtype, int32_t lay
     if (K < 1) K = 1;
     if (K > batch) K = batch;
     const int64_t nk = (batch + K - 1) / K;
+    PrefaultJob pfjob;   // (ends the prefault job on every return below)
+    {
+        const size_t oc = (size_t)batch * cells, rb = f64 ? 8 : 4, fb = f64 ? 8 : 1;
+        host_prefault(ctx, pfjob, {{rdm_out, rdm_out ? oc * rb : 0}, {flag_out, cfar ? oc * fb : 0},
+                                   {flagV_out, want_fv ? oc * fb : 0}});
+    }
     if (nk == 1 && zc_mode() != 0) {
         ht.mark();   // 1: set up
         bool taken = false;

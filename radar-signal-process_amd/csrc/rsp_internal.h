@@ -74,7 +74,6 @@ struct PcMfArgs {
     // output wraps.  nsub <= 1: the whole segment in one mf.nfft-point transform.
     int nsub, sub_step;
     const float* gain;   // fused iSTC (rsp_set_prefilter): echo column n scaled by gain[n], or null
-    int cpi_rows;        // PRT rows per CPI (dev-only -DRSP_XCD_AFFINITY block mapping)
     int nzero;
     int zero_lo[RSP_MAX_SEG + 1];
     int zero_hi[RSP_MAX_SEG + 1];
@@ -149,40 +148,6 @@ struct MtdArgs {
     CfarRArgs prev_cr;
 };
 
-// Persistent PC -> MTD (+ Doppler CFAR) -> range CFAR dataflow (rsp_set_flow, flow_kernel in
-// rsp_kernels.hip): one launch per call.  CPI c belongs to queue c % kFlowQueues (one per XCD);
-// a queue's items are PC units of its CPIs, MTD tiles (each carrying the range job of the
-// queue's previous CPI) and, after its last CPI, range-only items.  The PC rows of a CPI go to a
-// ring of kFlowSlots scratch slots per queue; hand-offs between workgroups are write-through
-// (sc1 stores, drained, one counter add per item) and read with sc1 loads.
-constexpr int kFlowQueues = 8;
-constexpr int kFlowSlots = 4;   // >= lead + 2 and >= lag + 2 (FlowArgs)
-constexpr int kFlowLine = 32;   // uint32 per control line (128 B)
-// control words: heads [kFlowQueues], counters [kFlowQueues][kFlowSlots][2] (PC units, MTD
-// tiles done), then the status line (a wait that timed out)
-constexpr int kFlowCtlLines = kFlowQueues + kFlowQueues * kFlowSlots * 2 + 1;
-struct FlowArgs {
-    const void* echo;      // [ncpi][P][R] (complex fp32 or fp16 I/Q)
-    PcMfArgs a1, a2;       // the short (FIR + MF) and the long matched-filter segment, rows = P
-    MtdArgs m;             // tile arguments (its per-launch pointers are unused)
-    CfarRArgs cr;          // range stage (cr.rflag && m.cv.enabled: range jobs run)
-    float2* ring;          // [kFlowQueues][kFlowSlots][P][R_out] PC rows
-    uint32_t* hring;       // [kFlowQueues][kFlowSlots][nm][region] Doppler hit lists
-    uint32_t* hcount;      // [kFlowQueues][kFlowSlots][nm]
-    float* rdm;            // [ncpi][V][R_out] output, or the RDM ring [kFlowQueues][kFlowSlots][V][R_out]
-    int rdm_ring;
-    uint8_t* flag;         // [ncpi][V][R_out] or null (no CFAR)
-    uint8_t* flagV;        // [ncpi][V][R_out] or null
-    uint32_t* ctl;         // kFlowCtlLines lines, zeroed before the launch
-    int ncpi;
-    int nl, nsh, nm;       // per CPI: long-row units, short-row groups, MTD tiles
-    int region;            // hit-list entries per tile
-    int order;             // 1: a block's PC units first, then its MTD tiles; 2: the two interleaved
-    int lead;              // block b holds the MTD tiles of CPI b and the PC units of CPI b + lead (1, 2)
-    int lag;               // the MTD tiles of CPI j carry the range jobs of CPI j - lag (1, 2)
-};
-bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams);
-hipError_t launch_flow(FlowArgs& a, int dtype, hipStream_t s);
 
 // Raw-data ingest (rsp_ingest.hip): one frame of uniform DDC PRT records.
 // motionParaMeasure.m's scalar arguments (rsp_measure_params, rsp_measure.hip).

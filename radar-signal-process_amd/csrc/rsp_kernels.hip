@@ -471,24 +471,8 @@ __device__ __forceinline__ void pc_mf_block(const TIn* __restrict__ echo, float2
     constexpr int M2 = N2 ? N2 : N1;
     using PC = PairCfg<N1, M2>;
     // unit u of a segment = (row u / nsub, overlap-save sub-block u % nsub)
-#ifdef RSP_XCD_AFFINITY
-    // (dev-only A/B of VERDICT r4 item 1b) the rows of CPI c go to blocks b with b % 8 == c % 8,
-    // i.e. to one XCD under round-robin dealing, where the MTD tiles of CPI c (same mapping in
-    // mtd_block) read them: chunks of a multiple of 8 CPIs, one segment-2 row per block
-    if constexpr (N2 != 0 && PC::RPB2 == 1) {
-        const int P = a2.cpi_rows, ncpi = a2.rows / (P > 0 ? P : 1);
-        if (P > 0 && ncpi % 8 == 0 && P % PC::RPB1 == 0 && a2.nsub <= 1 && a1.nsub <= 1) {
-            const int x = bid % 8, sl = bid / 8;
-            if (bid < nblk2) {
-                bid = (x + 8 * (sl / P)) * P + sl % P;
-            } else {
-                const int b = bid - nblk2, gpc = P / PC::RPB1;   // short-row groups per CPI
-                const int s2 = b / 8;
-                bid = nblk2 + (x + 8 * (s2 / gpc)) * gpc + s2 % gpc;
-            }
-        }
-    }
-#endif
+    // (CPI-to-XCD affinity of the rows was measured in round 5 and rejected:
+    //  profiles/r05/affinity/ab_record.txt; the build lives in the history, commit 0cf6ef3)
     if constexpr (N2 != 0) {
         if (bid < nblk2) {
             constexpr int G = PcCfg<N2>::G;
@@ -1379,14 +1363,6 @@ __device__ __forceinline__ void mtd_block(const float2* __restrict__ pc, float* 
                                           uint8_t* __restrict__ flagV, const MtdArgs& a, int bx, int by, int gx, int gy,
                                           unsigned char* smem, uint32_t* s_hits) {
     using C = MtdCfg<P, BEAMS>;
-#ifdef RSP_XCD_AFFINITY
-    // (dev-only, see pc_mf_block) the tiles of CPI c on blocks with linear id % 8 == c % 8
-    if (a.nwin == 0 && gy % 8 == 0 && gx % 8 == 0) {
-        const int lin = by * gx + bx, x = lin % 8, sl = lin / 8;
-        by = x + 8 * (sl / gx);
-        bx = sl % gx;
-    }
-#endif
     const size_t cpi = (size_t)by;
     const size_t R = (size_t)a.R_out;
     const size_t plane = (size_t)P * R;
@@ -1698,350 +1674,10 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
     }
 }
 
-// ================================================================== persistent dataflow
-// PC -> MTD (+ Doppler CFAR) -> range CFAR of a whole call in ONE launch (rsp_set_flow; VERDICT r4
-// item 1: the corner turn without launch boundaries).  FlowArgs (rsp_internal.h) describes the
-// queues.  Resident workgroups claim items from the queue of their own XCD (HW_REG_XCC_ID), so a
-// CPI's PC rows and its MTD tiles normally share one L2, and steal from the other queues once
-// theirs is drained (placement changes speed only: every hand-off is placement-independent).
-// Per queue (J CPIs, L = lead, D = lag) the item order is PC(0 .. L-1), then blocks b = 0 .. J-1
-// holding PC(b + L) and MTD(b) (PC first, or interleaved), then range-only items for the last D
-// CPIs.  Every dependency points to an earlier item of the same queue, and items are claimed in
-// queue order by running workgroups, so the smallest unfinished item can always run; the lead
-// and the lag keep each wait a block or more behind the item that satisfies it (a dependency on
-// the previous block waits for its slowest item):
-//   PC unit of CPI j      waits until MTD(j - S) is done with the scratch slot (S = kFlowSlots)
-//   MTD tile of CPI j     waits for PC(j) (all units) and MTD(j - D) (its range job reads that
-//                         CPI's RDM and hit list, written by every tile); slot reuse of the hit
-//                         list / RDM ring needs MTD(j - S + D), implied for S >= D + 2
-//   range-only item       waits for MTD(j) of its CPI
-// Hand-offs follow MI355X_MICROARCH.md's write-through form: every handed-off byte (PC rows, RDM,
-// flag background, hit lists and counts) is stored sc1, every storing wave drains vmcnt before
-// its workgroup's one relaxed counter add, and every load of such bytes is an sc1 load issued
-// after thread 0 saw the counter and the workgroup barrier.  Every wait is bounded (0.5 s; the
-// status word then records it and no later wait blocks), so a protocol fault ends the launch.
-// cache policies of the dataflow kernel's hand-off loads / stores (dev-only -D for timing A/B
-// only: anything but kSc1 breaks the hand-off protocol)
-#ifndef RSP_FLOW_LA
-#define RSP_FLOW_LA kSc1
-#endif
-#ifndef RSP_FLOW_SA
-#define RSP_FLOW_SA kSc1
-#endif
-#ifndef RSP_FLOW_PC_EARLY
-#define RSP_FLOW_PC_EARLY -1   // the long rows' spectrum loads: -1 as pc_row decides, 0 late, 1 early
-#endif
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
-    return v & (uint32_t)(kFlowQueues - 1);
-}
-__device__ __forceinline__ uint32_t* flow_head(uint32_t* ctl, int q) { return ctl + q * kFlowLine; }
-__device__ __forceinline__ uint32_t* flow_ctr(uint32_t* ctl, int q, int slot, int k) {
-    return ctl + (kFlowQueues + (q * kFlowSlots + slot) * 2 + k) * kFlowLine;
-}
-__device__ __forceinline__ uint32_t* flow_status(uint32_t* ctl) { return ctl + (kFlowCtlLines - 1) * kFlowLine; }
-
-// thread 0: wait until *p >= target (relaxed sc1 polls, s_sleep between)
-__device__ __forceinline__ void flow_wait(uint32_t* p, uint32_t target, uint32_t* st) {
-    if (ld_u32<kSc1>(p) >= target) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (ld_u32<kSc1>(p) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (ld_u32<kSc1>(st) != 0u) return;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s of the 100 MHz clock
-            __hip_atomic_fetch_or((gu32*)st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-    }
-}
-
-#ifdef RSP_DIAG_FLOW
-// Dev-only (-DRSP_DIAG_FLOW, tools/diag_flow.py): per workgroup, the first kFlowDiagItems items
-// as {kind | j << 4 | idx << 36, t0 claim decoded, t1 waits done, t2 published} on the 100 MHz
-// clock.
-constexpr int kFlowDiagWG = 1024, kFlowDiagItems = 512;
-__device__ uint64_t g_flow_diag[kFlowDiagWG * kFlowDiagItems * 4];
-#endif
-
-struct FlowItem {
-    int kind;   // 0 PC unit, 1 MTD tile, 2 range-only, -1 nothing (the PC of a CPI past the last)
-    int j;      // the CPI's index in its queue
-    int idx;    // unit / tile / region
-};
-
-__device__ __forceinline__ int flow_cpis(int ncpi, int q) {
-    return ncpi > q ? (ncpi - q + kFlowQueues - 1) / kFlowQueues : 0;
-}
-__device__ __forceinline__ uint32_t flow_total(const FlowArgs& a, int q, int nh) {
-    const int J = flow_cpis(a.ncpi, q);
-    const uint32_t npc = (uint32_t)(a.nl + a.nsh);
-    return J > 0 ? npc * (uint32_t)a.lead + (uint32_t)J * (npc + (uint32_t)a.nm) + (nh ? (uint32_t)a.lag * nh : 0u)
-                 : 0u;
-}
-__device__ __forceinline__ FlowItem flow_decode(const FlowArgs& a, int q, int nh, uint32_t k) {
-    const int J = flow_cpis(a.ncpi, q);
-    const uint32_t npc = (uint32_t)(a.nl + a.nsh), T = npc + (uint32_t)a.nm;
-    const uint32_t pro = npc * (uint32_t)a.lead;
-    if (k < pro) {   // the first `lead` CPIs' PC units
-        const int j = (int)(k / npc);
-        return j < J ? FlowItem{0, j, (int)(k % npc)} : FlowItem{-1, 0, 0};
-    }
-    k -= pro;
-    const uint32_t b = k / T, o = k % T;
-    if (b < (uint32_t)J) {
-        bool pc;
-        uint32_t i;
-        if (a.order == 2) {   // PC(b + lead) and MTD(b) dealt evenly through the block
-            const uint32_t p0 = o * npc / T, p1 = (o + 1) * npc / T;
-            pc = p1 > p0;
-            i = pc ? p0 : o - p0;
-        } else {
-            pc = o < npc;
-            i = pc ? o : o - npc;
-        }
-        if (pc) return (int)b + a.lead < J ? FlowItem{0, (int)b + a.lead, (int)i} : FlowItem{-1, 0, 0};
-        return FlowItem{1, (int)b, (int)i};
-    }
-    k -= (uint32_t)J * T;
-    if (nh == 0) return FlowItem{-1, 0, 0};
-    const int j = J - a.lag + (int)(k / (uint32_t)nh);   // range-only items of the last `lag` CPIs
-    return j >= 0 && j < J ? FlowItem{2, j, (int)(k % (uint32_t)nh)} : FlowItem{-1, 0, 0};
-}
-
-// The item's waits and body; returns the counter its completion publishes (null: none).  The
-// publishing itself (drain, barrier, counter add) is the caller's, at a fixed point of its loop.
-template <typename TIn, int N1, int N2, int P, int REF>
-__device__ __forceinline__ uint32_t* flow_item(const FlowArgs& a, int q, const FlowItem& it, int nh, unsigned char* smem,
-                                               uint32_t* s_hits, uint64_t* diag) {
-    auto stamp = [&](int k) {
-        if (diag && threadIdx.x == 0) diag[k] = __builtin_amdgcn_s_memrealtime();
-    };
-    using PC = PairCfg<N1, N2>;
-    constexpr int S = kFlowSlots;
-    const int j = it.j, c = q + kFlowQueues * j, slot = j % S;
-    const uint32_t gen = (uint32_t)(j / S);
-    uint32_t* st = flow_status(a.ctl);
-    const size_t R = (size_t)a.a2.R, Ro = (size_t)a.a2.R_out;
-    const size_t plane = (size_t)P * Ro;
-    const int npc = a.nl + a.nsh;
-    const bool hits_on = nh > 0;
-    auto rdm_of = [&](int jj) {
-        return a.rdm_ring ? a.rdm + (size_t)(q * S + jj % S) * plane : a.rdm + (size_t)(q + kFlowQueues * jj) * plane;
-    };
-    auto src_of = [&](int jj) {   // the range stage's view of CPI jj of this queue
-        const int ss = jj % S;
-        return RangeSrc{rdm_of(jj), a.flag ? a.flag + (size_t)(q + kFlowQueues * jj) * plane : nullptr,
-                        a.hring + (size_t)(q * S + ss) * a.nm * a.region, a.hcount + (size_t)(q * S + ss) * a.nm,
-                        a.region, a.cr};
-    };
-    if (it.kind == 0) {   // one PC unit: a long-segment row (sub-block), or RPB1 short-segment rows
-        if (threadIdx.x == 0 && j >= S) flow_wait(flow_ctr(a.ctl, q, slot, 1), gen * (uint32_t)a.nm, st);
-        __syncthreads();
-        stamp(2);
-        const TIn* ein = (const TIn*)a.echo + (size_t)c * P * R;
-        float2* pcs = a.ring + (size_t)(q * S + slot) * P * Ro;
-        float2* lds = reinterpret_cast<float2*>(smem);
-        if (it.idx < a.nl) {
-            constexpr int G = PcCfg<N2>::G;
-            const int ns = a.a2.nsub > 1 ? a.a2.nsub : 1;
-            pc_row<TIn, N2, G, kSc1, G == 64, RSP_FLOW_PC_EARLY>(ein, pcs, a.a2, it.idx / ns, tid_of<true>() % G, lds,
-                                                                 it.idx % ns);
-        } else {
-            constexpr int G = PcCfg<N1>::G;
-            const int tx = tid_of<true>();
-            const int grp = tx / G, ns = a.a1.nsub > 1 ? a.a1.nsub : 1;
-            const int u = (it.idx - a.nl) * PC::RPB1 + grp;
-            pc_row<TIn, N1, G, kSc1, G == 64>(ein, pcs, a.a1, u / ns, tx % G, lds + grp * PcCfg<N1>::SLOT,
-                                             u % ns);
-        }
-        return flow_ctr(a.ctl, q, slot, 0);
-    } else if (it.kind == 1) {   // one MTD tile (+ Doppler CFAR, hit list) + the range job of CPI j-1
-        const int D = a.lag;
-        if (threadIdx.x == 0) {
-            flow_wait(flow_ctr(a.ctl, q, slot, 0), (gen + 1) * (uint32_t)npc, st);
-            if (hits_on && j >= D) flow_wait(flow_ctr(a.ctl, q, (j - D) % S, 1), (uint32_t)((j - D) / S + 1) * a.nm, st);
-        }
-        __syncthreads();
-        stamp(2);
-        MtdTile T;
-        T.pc = a.ring + (size_t)(q * S + slot) * P * Ro;
-        T.rdm = rdm_of(j);
-        T.diff = nullptr;
-        T.flagV = a.flagV ? a.flagV + (size_t)c * plane : nullptr;
-        T.flag = a.flag ? a.flag + (size_t)c * plane : nullptr;
-        T.hits = hits_on ? a.hring + ((size_t)(q * S + slot) * a.nm + it.idx) * a.region : nullptr;
-        T.hit_count = hits_on ? a.hcount + (size_t)(q * S + slot) * a.nm + it.idx : nullptr;
-        T.cell_base = 0;
-        T.bx = it.idx;
-        // one tile instance: a tile without a job runs the hook with n == 0 (its gathers all out of
-        // range), so the kernel carries the MTD code once
-        const RangeSrc rs = src_of(j >= D ? j - D : j);
-        RangeJob57T<kSc1> rj;
-        const bool job = hits_on && j >= D;
-        if (job) rj.fetch_idx(rs, it.idx);
-        mtd_tile<P, REF, 1, RSP_FLOW_LA, RSP_FLOW_SA, RangeHookT<kSc1>, true>(T, a.m, smem, s_hits, RangeHookT<kSc1>{rj, rs});
-        if (job) {
-            rj.finish(rs);
-            if (rj.n > blockDim.x)
-                cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, it.idx, a.region, a.cr,
-                                            (int)(threadIdx.x + blockDim.x), (int)blockDim.x);
-        }
-        return flow_ctr(a.ctl, q, slot, 1);
-    } else if (it.kind == 2) {   // the last CPI's range stage: one hit region
-        if (threadIdx.x == 0) flow_wait(flow_ctr(a.ctl, q, slot, 1), (gen + 1) * (uint32_t)a.nm, st);
-        __syncthreads();
-        stamp(2);
-        const RangeSrc rs = src_of(j);
-        cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, it.idx, a.region, a.cr, (int)threadIdx.x,
-                                    (int)blockDim.x);
-    }
-    return nullptr;
-}
-
-// minimum waves per SIMD of the dataflow kernel (4 = four workgroups per CU, <= 128 VGPRs: the
-// residency of the chunked kernels; dev-only -D for A/B)
-#ifndef RSP_FLOW_WAVES
-#define RSP_FLOW_WAVES 4
-#endif
-template <typename TIn, int N1, int N2, int P, int REF>
-__global__ __launch_bounds__(kBlock, RSP_FLOW_WAVES) void flow_kernel(FlowArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t s_item, s_hits;
-    const int nh = (a.flag && a.cr.rflag && a.m.cv.enabled) ? a.nm : 0;
-    int h = (int)xcc_id();
-    if (threadIdx.x == 0)
-        s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-    int tried = 1;
-#ifdef RSP_DIAG_FLOW
-    int ndiag = 0;
-#endif
-    // Per item: decode, thread 0 waits for the item's inputs, barrier, body, thread 0 claims the
-    // next item, every wave drains its stores, barrier, thread 0 publishes the item and the next
-    // item number, barrier.  (Each thread-0 region is fenced by barriers: a block holding a barrier is
-    // never duplicated, so jump threading cannot join two thread-0 regions across the back edge --
-    // which splits the loop into nested loops with a divergent exit, and lanes 1-63 of wave 0
-    // then run the body's barriers without thread 0: tools/micro/handoff_probe.hip.)
-    for (;;) {
-        if (k >= flow_total(a, h, nh)) {   // this queue is drained: help the next one
-            if (tried == kFlowQueues) break;
-            ++tried;
-            h = (h + 1) % kFlowQueues;
-            __syncthreads();   // every thread has read s_item
-            if (threadIdx.x == 0)
-                s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-            continue;
-        }
-        // The item reads its arguments through an opaque copy of the kernarg pointer: otherwise
-        // hipcc hoists every field any item type uses into SGPRs for the whole loop (hundreds of
-        // SGPR spills into VGPR lanes, then VGPR spills).  The pointer stays constant-address-space,
-        // so the re-reads are scalar loads.
-        typedef const __attribute__((address_space(4))) FlowArgs FlowArgsK;
-        const FlowArgsK* ap = (const FlowArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ap));
-        const FlowArgs& ai = *(const FlowArgs*)ap;
-        const FlowItem it = flow_decode(ai, h, nh, k);
-        uint64_t* diag = nullptr;
-#ifdef RSP_DIAG_FLOW
-        if (blockIdx.x < (unsigned)kFlowDiagWG && ndiag < kFlowDiagItems) {
-            diag = g_flow_diag + ((size_t)blockIdx.x * kFlowDiagItems + ndiag) * 4;
-            if (threadIdx.x == 0) {
-                diag[0] = (uint64_t)(it.kind + 1) | ((uint64_t)(uint32_t)it.j << 4) | ((uint64_t)(uint32_t)it.idx << 36);
-                diag[1] = __builtin_amdgcn_s_memrealtime();
-            }
-        }
-        ++ndiag;
-#endif
-        uint32_t* sig = flow_item<TIn, N1, N2, P, REF>(ai, h, it, nh, smem, &s_hits, diag);
-        // claim the next item behind the item's last stores: the atomic's round trip overlaps the
-        // drain below (claimed earlier, its return would hold up the first vmcnt wait of the item)
-        uint32_t nxt = 0;
-        if (threadIdx.x == 0)
-            nxt = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifndef RSP_FLOW_NODRAIN   // (dev-only timing switch: publishing before the stores land is wrong)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done (sc1: in memory)
-#endif
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if (sig) __hip_atomic_fetch_add((gu32*)sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_item = nxt;
-        }
-#ifdef RSP_DIAG_FLOW
-        if (diag && threadIdx.x == 0) diag[3] = __builtin_amdgcn_s_memrealtime();
-#endif
-        __syncthreads();
-        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-    }
-}
-
-template <typename TIn, int N1, int N2, int P, int REF>
-static hipError_t launch_flow_t(FlowArgs& a, hipStream_t s) {
-    using PC = PairCfg<N1, N2>;
-    using MC = MtdCfg<P>;
-    static_assert(PC::T == kBlock && MC::T == kBlock, "flow items are 256-thread workgroups");
-    constexpr size_t lds = PC::lds > MC::template lds_for<REF>() ? PC::lds : MC::template lds_for<REF>();
-    static LaunchOnce once;
-    int resident = 0;
-    hipError_t e = launch_once(once, &resident, [&](int dev, int* v) {
-        hipError_t r = hipFuncSetAttribute((const void*)flow_kernel<TIn, N1, N2, P, REF>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (r != hipSuccess) return r;
-        int per = 0, cus = 0;
-        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)flow_kernel<TIn, N1, N2, P, REF>, kBlock,
-                                                         lds);
-        if (r != hipSuccess) return r;
-        r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        *v = per * cus;
-        return r;
-    });
-    if (e != hipSuccess) return e;
-    if (resident < 1) return hipErrorLaunchOutOfResources;
-    const int ns2 = a.a2.nsub > 1 ? a.a2.nsub : 1, ns1 = a.a1.nsub > 1 ? a.a1.nsub : 1;
-    a.nl = P * ns2;
-    a.nsh = (P * ns1 + PC::RPB1 - 1) / PC::RPB1;
-    a.nm = (a.a2.R_out + MC::W - 1) / MC::W;
-    a.region = MC::W * P;
-    const int64_t items = (int64_t)a.ncpi * (a.nl + a.nsh + a.nm) + (int64_t)kFlowQueues * (a.nl + a.nsh + a.nm);
-    const int grid = items < resident ? (int)items : resident;
-    hipLaunchKernelGGL((flow_kernel<TIn, N1, N2, P, REF>), dim3((unsigned)grid), dim3(kBlock), lds, s, a);
-    return hipGetLastError();
-}
-
-#ifdef RSP_DIAG_FLOW
-}  // namespace rsp
-// Dev-only diagnostic export (not in include/rsp.h): the dataflow kernel's item stamps.
-extern "C" int rsp_diag_flow(uint64_t* host, int64_t n) {
-    if (n < 0 || n > (int64_t)rsp::kFlowDiagWG * rsp::kFlowDiagItems * 4) return -1;
-    if (hipDeviceSynchronize() != hipSuccess) return -2;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsp::g_flow_diag), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
-               ? 0 : -3;
-}
-extern "C" int rsp_diag_flow_clear() {
-    static uint64_t zero[4096] = {};
-    for (size_t o = 0; o < sizeof(rsp::g_flow_diag); o += sizeof(zero))
-        if (hipMemcpyToSymbol(HIP_SYMBOL(rsp::g_flow_diag), zero, sizeof(zero), o, hipMemcpyHostToDevice) != hipSuccess)
-            return -1;
-    return 0;
-}
-namespace rsp {
-#endif
-
-bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams) {
-    return beams == 1 && P == 128 && nfft1 == 1024 && nfft2 == 4096 && (dtype == RSP_C64 || dtype == RSP_C32F16);
-}
-
-hipError_t launch_flow(FlowArgs& a, int dtype, hipStream_t s) {
-    if (a.ncpi <= 0) return hipSuccess;
-    if (!flow_supported(a.m.P, a.a1.mf.nfft, a.a2.mf.nfft, dtype, a.m.beams)) return hipErrorNotSupported;
-    if (a.m.cv.enabled && !(a.m.cv.ref == 5 && a.m.cv.save == 7)) return hipErrorNotSupported;
-    if (a.m.cv.enabled && a.cr.rflag && !(a.cr.ref == 5 && a.cr.save == 7)) return hipErrorNotSupported;
-    if (dtype == RSP_C64) return launch_flow_t<float2, 1024, 4096, 128, 5>(a, s);
-    return launch_flow_t<__half2, 1024, 4096, 128, 5>(a, s);
-}
+// (Round 5's persistent one-launch PC -> MTD dataflow, flow_kernel / rsp_set_flow, measured 82 %
+// of the chunked chain at c3 and left the product in round 6: DESIGN.md §7c / §7d; its source is
+// in the history, commit e3a7a73.  The sc1 (LA / SA) and opaque-index (OPQ) variants of the tile
+// and range-job templates above are what it instantiated.)
 
 // ================================================================== Doppler CFAR from an RDM
 // rsp_cfar's first stage: tile of W columns x V rows staged column-major in LDS.

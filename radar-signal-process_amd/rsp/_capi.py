@@ -27,13 +27,13 @@ RSP_WIN_KAISER, RSP_WIN_HAMMING, RSP_WIN_RECT = 0, 1, 2
 # Every exported symbol of include/rsp.h (checked by tests/test_capi_cpu.py)
 EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_set_chunk",
            "rsp_pc_mtd", "rsp_cfar", "rsp_pc_mtd_cfar", "rsp_pc_mtd_cfar_dev", "rsp_cfar_dev",
-           "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_set_streams",
+           "rsp_pc_dev", "rsp_profile", "rsp_profile_read", "rsp_profile_read_n", "rsp_set_streams",
            "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_set_host_pipeline", "rsp_ingest_record_bytes",
            "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter",
-           "rsp_set_flow", "rsp_flow_status", "rsp_pc_mtd_cfar_f64", "rsp_cfar_f64")
-RSP_NKERNELS = 5
-KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel", "flow_kernel")
+           "rsp_pc_mtd_cfar_f64", "rsp_cfar_f64")
+RSP_NKERNELS = 4
+KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
 
 
 class RspError(RuntimeError):
@@ -109,10 +109,6 @@ def load_library(path=None):
     lib.rsp_destroy.argtypes = [vp]
     lib.rsp_set_chunk.restype = C.c_int
     lib.rsp_set_chunk.argtypes = [vp, i64]
-    lib.rsp_set_flow.restype = C.c_int
-    lib.rsp_set_flow.argtypes = [vp, C.c_int32]
-    lib.rsp_flow_status.restype = C.c_int
-    lib.rsp_flow_status.argtypes = [vp, C.POINTER(C.c_int32)]
     lib.rsp_pc_mtd.restype = C.c_int
     lib.rsp_pc_mtd.argtypes = [vp, vp, i32, i32, i64, i64, i64, vp, i32]
     lib.rsp_cfar.restype = C.c_int
@@ -167,6 +163,8 @@ def load_library(path=None):
     lib.rsp_profile.argtypes = [vp, i32]
     lib.rsp_profile_read.restype = C.c_int
     lib.rsp_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    lib.rsp_profile_read_n.restype = C.c_int
+    lib.rsp_profile_read_n.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64), i32]
     _lib = lib
     return lib
 

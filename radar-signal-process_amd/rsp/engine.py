@@ -57,16 +57,6 @@ class Engine:
         """Chunk pipelines 1..4, or 0 for the library's mode-dependent default."""
         capi.check(self.lib.rsp_set_streams(self.ctx, int(n)), self.ctx)
 
-    def set_flow(self, mode):
-        """0: chunked two-pipeline chain; 1 / 2: one persistent dataflow launch (rsp_set_flow)."""
-        capi.check(self.lib.rsp_set_flow(self.ctx, int(mode)), self.ctx)
-
-    def flow_status(self):
-        """1 if a hand-off wait of the last dataflow launch hit its bound (synchronises)."""
-        t = C.c_int32(0)
-        capi.check(self.lib.rsp_flow_status(self.ctx, C.byref(t)), self.ctx)
-        return int(t.value)
-
     def set_chunk(self, cpis):
         capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)
 
@@ -295,7 +285,7 @@ class Engine:
         """{kernel name: (total ms, launches)} since profile(True)."""
         ms = (C.c_double * capi.RSP_NKERNELS)()
         n = (C.c_int64 * capi.RSP_NKERNELS)()
-        capi.check(self.lib.rsp_profile_read(self.ctx, ms, n), self.ctx)
+        capi.check(self.lib.rsp_profile_read_n(self.ctx, ms, n, capi.RSP_NKERNELS), self.ctx)
         return {capi.KERNEL_NAMES[k]: (ms[k], n[k]) for k in range(capi.RSP_NKERNELS) if n[k]}
 
     def cfar_dev(self, rdm, flag, flagV=None, cfar=None, stream=None):

@@ -58,4 +58,5 @@ if __name__ == "__main__":
     chain(64, 1024, 16, False, 13)
     chain(256, 8192, 4, False, 14)
     window(256, 8192, 4, 4, 15)
+    window(256, 8192, 8, 4, 17)   # 64 MiB of flags in one chunk: the flag memset path (c4's)
     chain(512, 16384, 2, True, 16)
