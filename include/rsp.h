@@ -52,7 +52,8 @@ extern "C" {
 #define RSP_ABI_VERSION 4   /* 2: rsp_set_fused / rsp_chain_check removed, rsp_set_pc_split added;
                                3: rsp_set_host_pipeline;
                                4: rsp_set_flow / rsp_flow_status (round 5's opt-in dataflow launch,
-                                  with its RSP_K_FLOW profile slot) removed; rsp_profile_read_n
+                                  with its RSP_K_FLOW profile slot) removed; rsp_set_range_concat
+                                  added; rsp_profile_read_n
                                   takes the arrays' length, rsp_profile_read writes exactly the 4
                                   ABI-3 entries */
 #define RSP_MAX_SEG 4
@@ -191,6 +192,15 @@ int rsp_set_chunk(rsp_ctx* ctx, int64_t cpis_per_chunk);
  * launch alone, for per-kernel timing). */
 int rsp_set_streams(rsp_ctx* ctx, int32_t n);
 
+/* Device memory a chain context holds (grow-only pools, freed by rsp_destroy), per call shape:
+ *   PC scratch        pipelines x chunk x beams x P x R_out x 8 B (c3: 2 x 16 x 128 x 4096 x 8 = 128 MiB)
+ *   hit-list slots    the grouped range stage keeps up to 16 chunks' Doppler-hit lists per
+ *                     pipeline, each MTD workgroup's region sized to its own cells (no overflow
+ *                     possible): pipelines x 16 x chunk x V x R_out x 4 B, capped at 1 GiB
+ *                     (c3: exactly 1 GiB; c5, one-CPI chunks: 2 x 16 x 32 MiB = 1 GiB)
+ *   host-call staging the host-buffer entry points' device copies of their inputs / outputs
+ * i.e. ~1.2 GiB per context at c3, against 288 GB of HBM; rsp_set_chunk scales all three. */
+
 /* ---- host-buffer entry points (MEX / fun_MTD_produce drop-in), synchronous ---------- */
 /* rsp_pc_mtd_cfar / rsp_pc_mtd take pageable host buffers (MATLAB's arrays).  A call that fits
  * one chunk (every MATLAB-granularity call) is staged through pinned memory that the kernels
@@ -280,6 +290,19 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
  * enable = 0 selects the whole-length transforms.  The threshold is fixed (4096 points).
  * RSP_ERR_UNSUPPORTED on a context without the specialised PC kernels (nothing to select). */
 int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable);
+
+/* Range concatenation between pulse compression and the MTD, replacing
+ *   Echo_0 = fun_lss_range_concate(prtNum, Echo_0)
+ * (MatlabProcess_xuzerui/fun_lss_range_concate.m:4-7, called at main.m:210-211 -- and commented
+ * out in the legacy fun_MTD_produce.m:70): after pulse compression, each row becomes the
+ * concatenation of its columns [src_start[i], src_start[i] + len[i]), i < nparts, in order; the
+ * MTD, the CFAR and every output then have R_out = sum(len) columns (rsp_pc_dev returns the
+ * concatenated rows, rsp_mtd_cfar_dev takes them).  The reference's ranges are
+ * {0, 89, 481} / {82, 236, 550} (1-based 1:82, 90:325, 482:1031 of the 1031 PC columns ->
+ * 868, the width fun_CFARflag's hard-coded 1:82 | 83:318 | 319:868 split assumes,
+ * main_cfar.m:143-145).  nparts = 0 restores the PC width.  Parts must lie inside the
+ * params' R_out columns; nparts <= RSP_MAX_SEG. */
+int rsp_set_range_concat(rsp_ctx* ctx, int32_t nparts, const int64_t* src_start, const int64_t* len);
 
 /* ---- raw-data ingest --------------------------------------------------- */
 /* One frame of the radar's PRT record stream -> DBF beams, replacing the per-PRT loop of

@@ -265,11 +265,29 @@ def fun_MTD_produce_v2(echo, params, pulses=None, zero_v_div=150):
     return mtd
 
 
-def fun_MTD_produce_legacy(echo, pulse2, pulse3):
+def fun_lss_range_concate(prtNum, s):
+    """MatlabProcess_xuzerui/fun_lss_range_concate.m:4-7, MATLAB's 1-based colons kept:
+    concate_range = zeros(prtNum, 868);
+    concate_range(:, 1:82)    = s(:, 1:82);
+    concate_range(:, 83:318)  = s(:, 83+(82-75):325);
+    concate_range(:, 319:868) = s(:, 325+(82+235-160):1031);"""
+    s = np.asarray(s)
+    out = np.zeros((prtNum, 868), s.dtype)
+    out[:, 1 - 1:82] = s[:, 1 - 1:82]
+    out[:, 83 - 1:318] = s[:, 83 + (82 - 75) - 1:325]
+    out[:, 319 - 1:868] = s[:, 325 + (82 + 235 - 160) - 1:1031]
+    return out
+
+
+def fun_MTD_produce_legacy(echo, pulse2, pulse3, concat=False):
     """MatlabProcess_xuzerui/fun_MTD_produce.m:3-126 (hard-coded 82/242/707 segments,
-    measured 75/160-sample pulses :54-60, no FIR circshift, no range concat)."""
+    measured 75/160-sample pulses :54-60, no FIR circshift; its range concat at :70 is commented
+    out).  concat=True: main.m's chain instead -- fun_lss_pulse_compression (:206),
+    fun_lss_range_concate (:210-211), then the same MTD and 0-v."""
     pc = fun_lss_pulse_compression(echo, pulse2, pulse3, 82, 242, echo.shape[1] - 324,
                                    fir_shift=False, offset2=75, offset3=160)
+    if concat:
+        pc = fun_lss_range_concate(pc.shape[0], pc)
     return fun_0v_pressing(fun_Process_MTD(pc), 150)
 
 

@@ -59,14 +59,7 @@ struct rsp_ctx {
     int64_t chunk = 0;  // 0 = default
     int nstreams = 0;   // chunk pipelines (the caller's stream + nstreams-1 internal ones); 0 = default
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
-    // (dev A/B, RSP_CU_SPLIT) PC and MTD on two CU-masked streams, chunk k's slot k % kSplitSlots
-    static constexpr int kSplitSlots = 3;
-    hipStream_t cm_pc = nullptr, cm_mtd = nullptr;
-    hipEvent_t ev_pd[kSplitSlots] = {}, ev_md[kSplitSlots] = {}, ev_sj = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
-    // flag-plane memset of big window chunks on a side stream, beside the chunk's PC
-    hipStream_t s_fm = nullptr;
-    hipEvent_t ev_fm0 = nullptr, ev_fm1 = nullptr;
     // The context's scratch (PC corner turn, hit lists, internal RDM, flagV staging) is reused by
     // every _dev call: a call's stream waits for the previous call's release event first, so
     // calls on different streams never overlap on it.
@@ -75,6 +68,13 @@ struct rsp_ctx {
     std::vector<void*> owned;           // constant tables (freed at destroy)
     std::map<int, float2*> tw;          // twiddle tables by length
     DevBuf scratch_pc, tmp_flagV, tmp_rdm;
+    // range concatenation between PC and MTD (rsp_set_range_concat, fun_lss_range_concate):
+    // PC rows are pc_w wide (the params' R_out); the MTD and every output see p.R_out = the sum
+    // of the ncat parts; cat_tmp holds the full-width PC rows of each pipeline
+    int64_t pc_w = 0;
+    int ncat = 0;
+    int64_t cat_src[RSP_MAX_SEG] = {}, cat_len[RSP_MAX_SEG] = {};
+    DevBuf cat_tmp;
     DevBuf pf_gain;                     // fused iSTC gains (rsp_set_prefilter)
     DevBuf hit_list;                    // per-lane Doppler-hit lists (fused range CFAR)
     DevBuf hit_ctr;                     // per-lane, per-MTD-workgroup hit counts
@@ -309,7 +309,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     if (!ctx) return RSP_OK;
     hipSetDevice(ctx->device);
     for (void* p : ctx->owned) hipFree(p);
-    DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
+    DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->cat_tmp, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
                       &ctx->meas_band, &ctx->ing_meta};
     for (DevBuf* b : bufs)
@@ -320,13 +320,6 @@ int rsp_destroy(rsp_ctx* ctx) {
     }
     for (int i = 0; i < 3; ++i) {
         if (ctx->aux[i]) hipStreamDestroy(ctx->aux[i]);
-    if (ctx->cm_pc) hipStreamDestroy(ctx->cm_pc);
-    if (ctx->cm_mtd) hipStreamDestroy(ctx->cm_mtd);
-    for (int i = 0; i < rsp_ctx::kSplitSlots; ++i) {
-        if (ctx->ev_pd[i]) hipEventDestroy(ctx->ev_pd[i]);
-        if (ctx->ev_md[i]) hipEventDestroy(ctx->ev_md[i]);
-    }
-    if (ctx->ev_sj) hipEventDestroy(ctx->ev_sj);
         if (ctx->ev_join[i]) hipEventDestroy(ctx->ev_join[i]);
     }
     {
@@ -355,9 +348,6 @@ int rsp_destroy(rsp_ctx* ctx) {
         h.pool.reset();
     }
     if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
-    if (ctx->s_fm) hipStreamDestroy(ctx->s_fm);
-    if (ctx->ev_fm0) hipEventDestroy(ctx->ev_fm0);
-    if (ctx->ev_fm1) hipEventDestroy(ctx->ev_fm1);
     if (ctx->ev_scratch) hipEventDestroy(ctx->ev_scratch);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -416,6 +406,7 @@ int rsp_create(rsp_ctx** out, int device, const rsp_params* prm) {
     rsp_ctx* ctx = new rsp_ctx();
     ctx->device = device;
     ctx->p = p;
+    ctx->pc_w = p.R_out;
     for (int s = 0; s < RSP_MAX_SEG; ++s) ctx->p.seg[s].coef_re = ctx->p.seg[s].coef_im = nullptr;
     auto bail = [&](int rc) {
         g_err = ctx->err;
@@ -848,7 +839,8 @@ static int scratch_release(rsp_ctx* ctx, hipStream_t s) {
     return RSP_OK;
 }
 
-static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s);
+static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s,
+                         int slot = 0);
 
 // Run one kernel launch, bracketed by HIP events on `s` when profiling is on (every
 // ctx->prof-th launch: a timing event costs the stream a few microseconds, so a sampled
@@ -873,7 +865,55 @@ static hipError_t timed(rsp_ctx* ctx, int k, hipStream_t s, F&& launch) {
     return hipEventRecord(e.b, s);
 }
 
-static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s) {
+static hipError_t run_pc_rows(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s);
+// Pulse compression of `rows` echo rows into `out` ([rows][R_out]).  With a range concatenation
+// (rsp_set_range_concat) the full-width PC rows land in cat_tmp slot `slot` (ensured by the caller:
+// slot * rows * pc_w complex per slot) and the parts are gathered into `out` by 2-D copies on s.
+static hipError_t run_pc(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s,
+                         int slot) {
+    if (ctx->ncat == 0) return run_pc_rows(ctx, ein, dtype, out, rows, s);
+    float2* full = (float2*)ctx->cat_tmp.p + (size_t)slot * rows * ctx->pc_w;
+    hipError_t e = run_pc_rows(ctx, ein, dtype, full, rows, s);
+    if (e != hipSuccess) return e;
+    const size_t so = sizeof(float2);
+    int64_t dst = 0;
+    for (int i = 0; i < ctx->ncat; ++i) {
+        e = hipMemcpy2DAsync(out + dst, (size_t)ctx->p.R_out * so, full + ctx->cat_src[i], (size_t)ctx->pc_w * so,
+                             (size_t)ctx->cat_len[i] * so, (size_t)rows, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+        dst += ctx->cat_len[i];
+    }
+    return hipSuccess;
+}
+static int cat_ensure(rsp_ctx* ctx, int slots, int64_t rows) {
+    return ctx->ncat ? ensure(ctx, ctx->cat_tmp, (size_t)slots * rows * ctx->pc_w * sizeof(float2)) : RSP_OK;
+}
+
+int rsp_set_range_concat(rsp_ctx* ctx, int32_t nparts, const int64_t* src_start, const int64_t* len) {
+    if (!ctx) return fail(nullptr, RSP_ERR_ARG, "rsp_set_range_concat: null ctx");
+    if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "rsp_set_range_concat: CFAR-only context");
+    if (nparts < 0 || nparts > RSP_MAX_SEG || (nparts > 0 && (!src_start || !len)))
+        return fail(ctx, RSP_ERR_ARG, "rsp_set_range_concat: bad part list (%d parts)", nparts);
+    int64_t w = 0;
+    for (int i = 0; i < nparts; ++i) {
+        if (len[i] < 1 || src_start[i] < 0 || src_start[i] + len[i] > ctx->pc_w)
+            return fail(ctx, RSP_ERR_ARG, "rsp_set_range_concat: part %d [%lld, +%lld) outside the %lld PC columns", i,
+                        (long long)src_start[i], (long long)len[i], (long long)ctx->pc_w);
+        w += len[i];
+    }
+    if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
+    HIP_TRY(ctx, hipDeviceSynchronize());   // no launch in flight still uses the old width
+    ctx->ncat = nparts;
+    for (int i = 0; i < nparts; ++i) {
+        ctx->cat_src[i] = src_start[i];
+        ctx->cat_len[i] = len[i];
+    }
+    ctx->p.R_out = nparts > 0 ? w : ctx->pc_w;
+    ctx->mtd.R_out = (int)ctx->p.R_out;
+    return RSP_OK;
+}
+
+static hipError_t run_pc_rows(rsp_ctx* ctx, const void* ein, int dtype, float2* out, int64_t rows, hipStream_t s) {
     if (!ctx->pc_v2)
         return timed(ctx, RSP_K_PC, s, [&] { return rsp::launch_pc(ein, dtype, out, rows, ctx->pc, ctx->pc_lds, s); });
     if (ctx->pc_mf.size() == 2 && rsp::pc_pair_supported(ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft)) {
@@ -932,8 +972,17 @@ int rsp_pc_dev(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t batch, v
     if (ctx->cfar_only) return fail(ctx, RSP_ERR_ARG, "context was created for CFAR only (params == NULL)");
     if (dtype != RSP_C64 && dtype != RSP_C32F16) return fail(ctx, RSP_ERR_ARG, "rsp_pc_dev: dtype %d", dtype);
     if (!set_device(ctx)) return fail(ctx, RSP_ERR_HIP, "hipSetDevice failed");
-    HIP_TRY(ctx, run_pc(ctx, d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, (hipStream_t)stream));
-    return RSP_OK;
+    if (ctx->ncat == 0) {
+        HIP_TRY(ctx, run_pc(ctx, d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, (hipStream_t)stream));
+        return RSP_OK;
+    }
+    // the concatenation stages full-width rows in the context's scratch
+    hipStream_t s = (hipStream_t)stream;
+    int rc = scratch_acquire(ctx, s);
+    if (rc) return rc;
+    if ((rc = cat_ensure(ctx, 1, batch * ctx->p.P))) return rc;
+    HIP_TRY(ctx, run_pc(ctx, d_echo, dtype, (float2*)d_pc, batch * ctx->p.P, s));
+    return scratch_release(ctx, s);
 }
 
 int rsp_set_pc_split(rsp_ctx* ctx, int32_t enable) {
@@ -997,32 +1046,6 @@ static int range_group() {
     return g;
 }
 
-// (dev A/B of VERDICT r5 item 1) RSP_CU_SPLIT=n: PC launches on a stream whose CU mask holds bits
-// [0, 8n) -- the mask bits spread over the XCDs (tools/micro/cumask_probe.hip) -- and the MTD and
-// range launches on a stream with the other bits, chained by events through kSplitSlots scratch
-// slots (PC(k) waits for MTD(k - slots); MTD(k) waits for PC(k)).  Not the product schedule.
-static int cu_split() {
-    static const int n = [] { const char* v = getenv("RSP_CU_SPLIT"); return v && *v ? atoi(v) : 0; }();
-    return n;
-}
-static int split_streams(rsp_ctx* ctx) {
-    if (ctx->cm_pc) return RSP_OK;
-    int ncu = 0;
-    HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    const int words = (ncu + 31) / 32, npc = 8 * cu_split();
-    if (npc <= 0 || npc >= ncu) return fail(ctx, RSP_ERR_ARG, "RSP_CU_SPLIT=%d: %d of %d CUs", cu_split(), npc, ncu);
-    std::vector<uint32_t> mp((size_t)words, 0u), mm((size_t)words, 0u);
-    for (int b = 0; b < ncu; ++b) (b < npc ? mp : mm)[(size_t)(b / 32)] |= 1u << (b % 32);
-    HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->cm_pc, (uint32_t)words, mp.data()));
-    HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->cm_mtd, (uint32_t)words, mm.data()));
-    for (int i = 0; i < rsp_ctx::kSplitSlots; ++i) {
-        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_pd[i], hipEventDisableTiming));
-        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_md[i], hipEventDisableTiming));
-    }
-    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_sj, hipEventDisableTiming));
-    return RSP_OK;
-}
-
 static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
                           const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
                           float* d_diff, hipStream_t s, bool pc_input) {
@@ -1062,15 +1085,13 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     std::vector<int64_t> cstart{0};
     while (cstart.back() < units) cstart.push_back(cstart.back() + cu < units ? cstart.back() + cu : units);
     const int64_t nchunks = (int64_t)cstart.size() - 1;
-    const bool split = cu_split() > 0 && win == 0 && !pc_input;
-    const int ns = split ? 1 : (int)(nsd < nchunks ? nsd : nchunks);
-    const int pslots = split ? rsp_ctx::kSplitSlots : ns;   // PC scratch slots
+    const int ns = (int)(nsd < nchunks ? nsd : nchunks);
     const size_t plane = (size_t)V * Ro;                  // output cells per CPI
     const size_t cells = (size_t)cu * ocpi * plane;       // output cells per chunk slot
     const size_t pcrows = (size_t)(cu + (win > 0 ? 1 : 0)) * NB * P;
-    int rc = pc_input ? RSP_OK : ensure(ctx, ctx->scratch_pc, (size_t)pslots * pcrows * Ro * sizeof(float2));
+    int rc = pc_input ? RSP_OK : ensure(ctx, ctx->scratch_pc, (size_t)ns * pcrows * Ro * sizeof(float2));
     if (rc) return rc;
-    if (split && (rc = split_streams(ctx))) return rc;
+    if (!pc_input && (rc = cat_ensure(ctx, ns, (int64_t)pcrows))) return rc;
     int nreg = 0, reg = 0;
     if (cfar) {
         // fused range stage: per-lane hit lists, one region per MTD workgroup sized to its
@@ -1116,27 +1137,13 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     const bool fm = cfar && cr.rflag && d_flag &&
                     (fenv >= 0 ? fenv == 1 : (V >= 256 && (uint64_t)cells >= (64ull << 20)));
     if (fm) m.flag_zero = 0;
-    // ... on a side stream that forks from the lane before the chunk's PC and joins it before the
-    // MTD, so the fill runs beside the PC instead of between PC and MTD (c4's
-    // ~45 us memset per step).  Dev A/B: RSP_FLAG_MEMSET_SIDE=0 puts it back on the lane.
-    static const int fside = [] { const char* v = getenv("RSP_FLAG_MEMSET_SIDE"); return v && *v ? atoi(v) : 1; }();
-    const bool fms = fm && fside != 0 && !pc_input;
-    if (fms && !ctx->s_fm) {
-        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->s_fm, hipStreamNonBlocking));
-        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fm0, hipEventDisableTiming));
-        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fm1, hipEventDisableTiming));
-    }
+    // (The fill on a side stream beside the chunk's PC, joined before the MTD, measured the same:
+    // c4 133.8k vs 134.2k windows/s, three interleaved pairs, bit-identical -- the fill and the
+    // PC share the HBM; profiles/r06/c4/flag_memset_side.txt.)
     // Chunk k runs on lane k % ns (lane 0 = the caller's stream), each lane with its own
     // scratch slot, so PC of one chunk overlaps MTD / CFAR of the previous one.  The lanes
     // fork from and join back into the caller's stream.
     hipStream_t lanes[4] = {s, nullptr, nullptr, nullptr};
-    if (split) {   // fork both masked streams from the caller's; lane 0 = the MTD stream
-        if (!ctx->ev_fork) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-        HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
-        HIP_TRY(ctx, hipStreamWaitEvent(ctx->cm_pc, ctx->ev_fork, 0));
-        HIP_TRY(ctx, hipStreamWaitEvent(ctx->cm_mtd, ctx->ev_fork, 0));
-        lanes[0] = ctx->cm_mtd;
-    }
     if (ns > 1) {
         if (!ctx->ev_fork) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
@@ -1174,23 +1181,8 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         if (pc_input) {   // d_echo already holds pulse-compressed rows [units][beams][P][R_out]
             pcs = (float2*)d_echo + (size_t)u0 * NB * P * Ro;
         } else {
-            if (fms) {   // the flag fill of this chunk beside its PC (the lane's earlier work is done with it)
-                HIP_TRY(ctx, hipEventRecord(ctx->ev_fm0, ls));
-                HIP_TRY(ctx, hipStreamWaitEvent(ctx->s_fm, ctx->ev_fm0, 0));
-                HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ctx->s_fm));
-                HIP_TRY(ctx, hipEventRecord(ctx->ev_fm1, ctx->s_fm));
-            }
-            if (split) {
-                const int sl = (int)(k % rsp_ctx::kSplitSlots);
-                pcs = (float2*)ctx->scratch_pc.p + sl * pcrows * Ro;
-                if (k >= rsp_ctx::kSplitSlots) HIP_TRY(ctx, hipStreamWaitEvent(ctx->cm_pc, ctx->ev_md[sl], 0));
-                HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, n * NB * P, ctx->cm_pc));
-                HIP_TRY(ctx, hipEventRecord(ctx->ev_pd[sl], ctx->cm_pc));
-                HIP_TRY(ctx, hipStreamWaitEvent(ls, ctx->ev_pd[sl], 0));
-            } else {
-                pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
-                HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls));
-            }
+            pcs = (float2*)ctx->scratch_pc.p + lane * pcrows * Ro;
+            HIP_TRY(ctx, run_pc(ctx, ein, dtype, pcs, (n + (win > 0 ? 1 : 0)) * NB * P, ls, lane));
         }
         m.diff = d_diff ? d_diff + o0 : nullptr;
         m.prev_nregions = 0;
@@ -1211,8 +1203,7 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
                 m.prev_cr = cr;
             }
         }
-        if (fms) HIP_TRY(ctx, hipStreamWaitEvent(ls, ctx->ev_fm1, 0));
-        else if (fm) HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ls));
+        if (fm) HIP_TRY(ctx, hipMemsetAsync(d_flag + o0, 0, (size_t)ncpi * plane, ls));
         HIP_TRY(ctx, timed(ctx, RSP_K_MTD, ls, [&] { return rsp::launch_mtd(pcs, rdm, fv, (int)ncpi, m, ls); }));
         if (cfar && cr.rflag) {
             Pending& pv = pend[lane];
@@ -1239,7 +1230,6 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
                 pv.nreg = 0;
             }
         }
-        if (split) HIP_TRY(ctx, hipEventRecord(ctx->ev_md[(int)(k % rsp_ctx::kSplitSlots)], ls));
     }
     for (int lane = 0; lane < ns; ++lane) {   // each lane's last chunk
         const Pending& pv = pend[lane];
@@ -1251,10 +1241,6 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
     for (int i = 1; i < ns; ++i) {
         HIP_TRY(ctx, hipEventRecord(ctx->ev_join[i - 1], lanes[i]));
         HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join[i - 1], 0));
-    }
-    if (split) {   // join: the MTD stream's last work follows every PC; the caller's stream waits for it
-        HIP_TRY(ctx, hipEventRecord(ctx->ev_sj, ctx->cm_mtd));
-        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_sj, 0));
     }
     return RSP_OK;
 }

@@ -31,7 +31,7 @@ EXPORTS = ("rsp_version", "rsp_create", "rsp_destroy", "rsp_last_error", "rsp_se
            "rsp_create_v2", "rsp_create_legacy", "rsp_window_pc_mtd_cfar_dev", "rsp_pc_mtd_cfar_diff_dev",
            "rsp_mtd_cfar_dev", "rsp_set_pc_split", "rsp_set_host_pipeline", "rsp_ingest_record_bytes",
            "rsp_ingest_ddc_dev", "rsp_ingest_frame_dev", "rsp_motion_measure_dev", "rsp_prefilter_dev", "rsp_set_prefilter",
-           "rsp_pc_mtd_cfar_f64", "rsp_cfar_f64")
+           "rsp_pc_mtd_cfar_f64", "rsp_cfar_f64", "rsp_set_range_concat")
 RSP_NKERNELS = 4
 KERNEL_NAMES = ("pc_kernel", "mtd_kernel", "cfar_r_kernel", "cfar_v_kernel")
 
@@ -163,6 +163,8 @@ def load_library(path=None):
     lib.rsp_profile.argtypes = [vp, i32]
     lib.rsp_profile_read.restype = C.c_int
     lib.rsp_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    lib.rsp_set_range_concat.restype = C.c_int
+    lib.rsp_set_range_concat.argtypes = [vp, i32, C.POINTER(i64), C.POINTER(i64)]
     lib.rsp_profile_read_n.restype = C.c_int
     lib.rsp_profile_read_n.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64), i32]
     _lib = lib

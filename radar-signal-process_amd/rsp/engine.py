@@ -30,6 +30,8 @@ class Engine:
         capi.check(rc, None)
         self.ctx = ctx
         self.device = device
+        if spec is not None and spec.concat:
+            self.set_range_concat(spec.concat)
         if chunk:
             self.set_chunk(chunk)
         if streams:
@@ -56,6 +58,14 @@ class Engine:
     def set_streams(self, n):
         """Chunk pipelines 1..4, or 0 for the library's mode-dependent default."""
         capi.check(self.lib.rsp_set_streams(self.ctx, int(n)), self.ctx)
+
+    def set_range_concat(self, parts):
+        """fun_lss_range_concate between PC and MTD: [(src_start, len), ...] of the PC columns
+        (rsp_set_range_concat); [] restores the PC width.  The spec's R_out must match."""
+        n = len(parts)
+        src = (C.c_int64 * max(n, 1))(*[int(a) for a, _ in parts])
+        ln = (C.c_int64 * max(n, 1))(*[int(b) for _, b in parts])
+        capi.check(self.lib.rsp_set_range_concat(self.ctx, n, src, ln), self.ctx)
 
     def set_chunk(self, cpis):
         capi.check(self.lib.rsp_set_chunk(self.ctx, int(cpis)), self.ctx)

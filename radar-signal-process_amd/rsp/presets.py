@@ -106,6 +106,10 @@ class Spec:
     mtd_nfft: int = 0          # Doppler FFT length V (0 = P); DMX: 2048 over 1536 pulses
     beams: int = 1             # 2: DMX left/right pair, RDM = |X_L| + |X_R|
     zero_ends: int = 0         # DMX zeroSetFlagMTD: MTD_0_num + 1 (0 = fun_0v_pressing instead)
+    # range concatenation between PC and MTD (fun_lss_range_concate, rsp_set_range_concat):
+    # [(src_start, len), ...] of the pc_width PC columns; R_out is then their total
+    concat: list = field(default_factory=list)
+    pc_width: int = 0          # PC output columns (rsp_params.R_out); 0 = R_out
 
     @property
     def V(self):
@@ -115,7 +119,7 @@ class Spec:
     def to_c(self):
         """Build the ctypes rsp_params; returns (struct, keepalive list)."""
         prm = capi.rsp_params()
-        prm.P, prm.R, prm.R_out = self.P, self.R, self.R_out
+        prm.P, prm.R, prm.R_out = self.P, self.R, self.pc_width or self.R_out
         prm.nseg = len(self.segments)
         prm.window, prm.window_beta = self.window, self.window_beta
         prm.fftshift, prm.zero_v_div = self.fftshift, self.zero_v_div
@@ -172,9 +176,16 @@ def v2(P=332, R=3404, point_prt=None, radar=None):
                     fir_shift=fir_group_delay(FIR_TAPS), radar=rp)
 
 
-def legacy(P=1536, R=1031):
+# fun_lss_range_concate (MatlabProcess_xuzerui/fun_lss_range_concate.m:4-7): columns 1:82,
+# 83+(82-75):325 and 325+(82+235-160):1031 (1-based) of the 1031 PC columns -> 868
+LEGACY_CONCAT = [(0, 82), (89, 236), (481, 550)]
+
+
+def legacy(P=1536, R=1031, concat=False):
     """MatlabProcess_xuzerui/fun_MTD_produce.m:3-126 (hard-coded 82/242/707, measured pulses,
-    fc 5.5 GHz, PRT 64.88 us :24-38)."""
+    fc 5.5 GHz, PRT 64.88 us :24-38).  concat=True: main.m's chain, which concatenates the
+    range segments between pulse compression and MTD (main.m:210-211, fun_lss_range_concate;
+    commented out inside fun_MTD_produce.m:70): the MTD and CFAR then see 868 columns."""
     rp = dict(prtNum=P, fs=25e6, fc=5500e6, prt=64.88e-6, B=10e6,
               point_prt=[R, 82, 242, R - 324])
     rp["prf"] = 1.0 / rp["prt"]
@@ -183,6 +194,13 @@ def legacy(P=1536, R=1031):
                     load_data("legacy_pulse3"), fir_shift=0, radar=rp)
     # fun_CFARflag's hard-coded split after fun_lss_range_concate (main_cfar.m:143-145)
     spec.cfar_segments = [(0, 82), (82, 318), (318, min(868, R))]
+    if concat:
+        if R != 1031:
+            raise ValueError("fun_lss_range_concate indexes the 1031-column legacy row (got R=%d)" % R)
+        spec.concat = list(LEGACY_CONCAT)
+        spec.pc_width = R
+        spec.R_out = sum(n for _, n in LEGACY_CONCAT)
+        spec.name = "legacy_concat"
     return spec
 
 
@@ -237,12 +255,15 @@ def dmx_native_cfar(spec, T=7.0):
     return Cfar(TR=T, TV=T, M0=spec.radar["M0"], zero_v_div=0, segments=list(spec.cfar_segments))
 
 
-PRESETS = {"v2": v2, "legacy": legacy, "dmx": dmx, "dmx_native": dmx_native}
+PRESETS = {"v2": v2, "legacy": legacy, "legacy_concat": lambda P, R: legacy(P, R, concat=True), "dmx": dmx,
+           "dmx_native": dmx_native}
 
 
 def make(name, P, R):
     if name == "legacy":
         return legacy(P, R)
+    if name == "legacy_concat":
+        return legacy(P, R, concat=True)
     if name == "dmx_native":
         return dmx_native(P, R)
     return PRESETS[name](P, R)

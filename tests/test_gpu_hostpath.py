@@ -247,3 +247,35 @@ def test_one_chunk_two_beam(torch_cuda):
     rdm2, flag2, _ = eng.pc_mtd_cfar(e, cf, want_flagV=False)
     assert np.array_equal(rdm2, want[0]) and np.array_equal(flag2, want[1])
     eng.close()
+
+
+def test_cfar_f64_dma_fallback_matches_cfar(torch_cuda):
+    """rsp_cfar_f64 beyond the one-chunk limit (more than kParts = 16 output parts: batch 20 with
+    flagV) takes the DMA pipeline instead of pinned staging: the double RDM narrowed by the copy
+    threads on its way into the pinned input ring (h2d_pieces narrow 2), the u8 flag transposes for
+    MATLAB's layout, and the flags widened to double as their pieces land (d2h widen 2).  Both
+    layouts, bit-exact against rsp_cfar on the same (float-representable) values."""
+    import ctypes as C
+    from rsp import _capi as capi
+    from rsp import presets
+    from rsp.engine import Engine
+    eng = Engine(presets.v2(64, 1024))
+    cf = presets.default_cfar(eng.spec)
+    cp = cf.to_c()
+    lib = eng.lib
+    V, R, B = 64, 1024, 20
+    rng = np.random.default_rng(77)
+    rdm = np.abs(rng.standard_normal((B, V, R)) + 1j * rng.standard_normal((B, V, R))).astype(np.float32)
+    rdm[:, 20, 300] = 60.0
+    rdm[:, 45, 700:703] = [30.0, 40.0, 35.0]
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    for lay in (capi.RSP_ROWMAJOR, capi.RSP_COLMAJOR):
+        x = rdm if lay == capi.RSP_ROWMAJOR else np.ascontiguousarray(np.swapaxes(rdm, 1, 2))
+        f8, v8 = np.empty(x.shape, np.uint8), np.empty(x.shape, np.uint8)
+        assert lib.rsp_cfar(eng.ctx, ptr(x), lay, V, R, B, C.byref(cp), ptr(f8), ptr(v8)) == 0
+        x64 = x.astype(np.float64)
+        f64, v64 = np.full(x.shape, 7.0), np.full(x.shape, 7.0)
+        assert lib.rsp_cfar_f64(eng.ctx, ptr(x64), lay, V, R, B, C.byref(cp), ptr(f64), ptr(v64)) == 0
+        assert np.array_equal(f64, f8.astype(np.float64)) and np.array_equal(v64, v8.astype(np.float64))
+        assert v8.sum() > 0
+    eng.close()

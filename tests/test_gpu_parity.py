@@ -394,3 +394,69 @@ def test_range_groups_across_group_boundaries(torch_cuda):
     for r, f in outs[1:]:
         np.testing.assert_array_equal(r, outs[0][0])
         np.testing.assert_array_equal(f, outs[0][1])
+
+
+# ---------------------------------------------------------------- fun_lss_range_concate (main.m)
+def test_legacy_range_concat_chain(torch_cuda):
+    """main.m's legacy simulation chain (MatlabProcess_xuzerui/main.m:206-211): PC, then
+    fun_lss_range_concate (fun_lss_range_concate.m:4-7: 1031 -> 868 columns), then MTD + 0-v and
+    fun_CFARflag's 1:82 | 83:318 | 319:868 split (main_cfar.m:143-145), which assumes the 868
+    columns.  rsp_set_range_concat gathers the PC columns between PC and MTD: the RDM against the
+    numpy oracle of the concatenated chain, CFAR flags against the oracle's, and -- the gather
+    being a copy -- bit-exact against PC without concat, gathered, then MTD / CFAR of those rows."""
+    torch = torch_cuda
+    from rsp import presets
+    from rsp.engine import Engine
+    P, R, B = 96, 1031, 2
+    spec = presets.legacy(P, R, concat=True)
+    assert spec.R_out == 868 and spec.cfar_segments[-1] == (318, 868)
+    cf = presets.default_cfar(spec)
+    eng = Engine(spec)
+    echo = _echo(eng, B, seed=1211)
+    d_in = torch.from_numpy(echo).cuda()
+    shp = (B, P, 868)
+    d_rdm = torch.empty(shp, dtype=torch.float32, device="cuda")
+    d_flag = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.run_dev(d_in, rdm=d_rdm, flag=d_flag, cfar=cf)
+    torch.cuda.synchronize()
+    p2, p3 = presets.load_data("legacy_pulse2"), presets.load_data("legacy_pulse3")
+    want = np.stack([ref.fun_MTD_produce_legacy(x.astype(np.complex128), p2, p3, concat=True) for x in echo])
+    got = d_rdm.cpu().numpy()
+    assert rel_err(got, want) < RDM_TOL
+    flag, _, amb = oracle_flags(want, cf)
+    hard, soft = flag_mismatch(d_flag.cpu().numpy(), flag, amb)
+    assert hard == 0 and soft <= 2, (hard, soft)
+    assert flag.sum() > 0
+    # PC alone returns the concatenated rows = the plain legacy PC rows gathered (bit-exact)
+    plain = Engine(presets.legacy(P, R))
+    pc_full = torch.empty((B, P, R), dtype=torch.complex64, device="cuda")
+    plain.pc_dev(d_in, pc_full)
+    pc_cat = torch.empty((B, P, 868), dtype=torch.complex64, device="cuda")
+    eng.pc_dev(d_in, pc_cat)
+    torch.cuda.synchronize()
+    gathered = torch.cat([pc_full[..., a:a + n] for a, n in presets.LEGACY_CONCAT], dim=-1).contiguous()
+    assert torch.equal(pc_cat, gathered)
+    # the MTD / CFAR stage on those rows (rsp_mtd_cfar_dev) gives the chain's outputs exactly
+    r2 = torch.empty(shp, dtype=torch.float32, device="cuda")
+    f2 = torch.empty(shp, dtype=torch.uint8, device="cuda")
+    eng.mtd_dev(gathered, rdm=r2, flag=f2, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(r2, d_rdm) and torch.equal(f2, d_flag)
+    # host API (MATLAB layout) through the same context: identical
+    rdm_h, flag_h, _ = eng.pc_mtd_cfar(echo, cf)
+    assert np.array_equal(rdm_h, got) and np.array_equal(flag_h, d_flag.cpu().numpy())
+    # a part outside the PC row is refused; no parts restores the PC width (the plain legacy chain)
+    from rsp import _capi as capi
+    import ctypes as C
+    bad = (C.c_int64 * 1)(1000), (C.c_int64 * 1)(100)
+    assert eng.lib.rsp_set_range_concat(eng.ctx, 1, bad[0], bad[1]) == capi.RSP_ERR_ARG
+    eng.set_range_concat([])
+    eng.spec = presets.legacy(P, R)
+    r3 = torch.empty((B, P, R), dtype=torch.float32, device="cuda")
+    eng.run_dev(d_in, rdm=r3)
+    r4 = torch.empty((B, P, R), dtype=torch.float32, device="cuda")
+    plain.run_dev(d_in, rdm=r4)
+    torch.cuda.synchronize()
+    assert torch.equal(r3, r4)
+    eng.close()
+    plain.close()

@@ -228,3 +228,20 @@ def test_c_oracle_matches_numpy_oracle_at_checker_sizes(name, P, R):
     np.testing.assert_array_equal(fc[0], f)
     np.testing.assert_array_equal(fvc[0], fv)
     assert f.sum() > 0
+
+
+def test_range_concate_restatement():
+    """fun_lss_range_concate (MatlabProcess_xuzerui/fun_lss_range_concate.m:4-7) keeps MATLAB's
+    1-based colons; the preset's 0-based (start, len) parts (what rsp_set_range_concat gathers)
+    select the same columns: 1:82, 90:325, 482:1031 -> 868."""
+    from rsp import presets
+    rng = np.random.default_rng(5)
+    s = rng.standard_normal((7, 1031)) + 1j * rng.standard_normal((7, 1031))
+    c = ref.fun_lss_range_concate(7, s)
+    assert c.shape == (7, 868)
+    g = np.concatenate([s[:, a:a + n] for a, n in presets.LEGACY_CONCAT], axis=1)
+    assert np.array_equal(c, g)
+    assert np.array_equal(c[:, 82], s[:, 89]) and np.array_equal(c[:, 317], s[:, 324])
+    assert np.array_equal(c[:, 318], s[:, 481]) and np.array_equal(c[:, 867], s[:, 1030])
+    spec = presets.legacy(48, 1031, concat=True)
+    assert spec.R_out == 868 and spec.pc_width == 1031 and spec.cfar_segments == [(0, 82), (82, 318), (318, 868)]

@@ -20,19 +20,7 @@ for what in "$@"; do
     probe)
       timeout -k 10 90 tools/micro/handoff_probe ${PROBE_ROUNDS:-64} > gpurun_out/handoff_probe.txt 2>&1; rc=$?
       cat gpurun_out/handoff_probe.txt; [ $rc -eq 0 ] || exit $rc ;;
-    flowtest)
-      timeout -k 10 300 python -u -m pytest tests/test_gpu_flow.py -x -v --timeout 120 --timeout-method thread \
-          > gpurun_out/pytest_flow.log 2>&1; rc=$?
-      echo "flow tests rc=$rc"; grep -E "PASS|FAIL|Error|error" gpurun_out/pytest_flow.log | tail -20; [ $rc -eq 0 ] || exit $rc ;;
-    flowab)
-      # the schedules interleaved on one box: FLOWS (default "0 1 2") x REPS, config CFG (default c3)
-      for i in $(seq ${REPS:-2}); do
-        for f in ${FLOWS:-0 1 2}; do
-          timeout -k 10 200 python bench.py --config ${CFG:-c3} --steps ${STEPS:-20} --cpu-seconds 0 --flow $f ${BENCH_ARGS:-} \
-              > gpurun_out/flowab_${f}.log 2>&1 || { echo "bench flow=$f failed"; tail -5 gpurun_out/flowab_${f}.log; exit 1; }
-          python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print('flow', sys.argv[2], d['value'], d['ms_per_step'], {k: v['avg_us'] for k, v in r.get('kernels', {}).items()})" gpurun_out/flowab_${f}.log $f
-        done
-      done ;;
+    # (flowtest / flowab: round 5's dataflow-kernel cases; the kernel left the product in round 6)
     digest)
       DIGEST=1 CONFIGS=none REPS=0 bash tools/ab2.sh || exit $? ;;
     ab)
