@@ -13,6 +13,13 @@ def rel_err(a, b):
     return float(np.linalg.norm(np.asarray(a, np.float64) - b) / np.linalg.norm(b))
 
 
+MAX_TOL = 1e-5        # max|RDM_gpu - RDM_ref| / max|RDM_ref|   (SURVEY.md §8d's second figure)
+
+
+def max_rel(a, b):
+    return float(np.max(np.abs(np.asarray(a, np.float64) - b)) / np.max(np.abs(b)))
+
+
 def oracle_cfar_dict(spec_cfar):
     d = spec_cfar.as_dict()
     d["zero_v_div"] = spec_cfar.zero_v_div

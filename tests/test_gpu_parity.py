@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import rsp_ref as ref
-from _util import NEAR_TOL, RDM_TOL, flag_mismatch, oracle_flags, oracle_flags_c, oracle_rdm, rel_err
+from _util import MAX_TOL, NEAR_TOL, RDM_TOL, flag_mismatch, max_rel, oracle_flags, oracle_flags_c, oracle_rdm, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -103,6 +103,7 @@ def test_pc_mtd_parity(torch_cuda, name, P, R, batch):
     want = oracle_rdm(name, echo)
     err = rel_err(got, want)
     assert err < RDM_TOL, err
+    assert max_rel(got, want) < MAX_TOL, max_rel(got, want)
     # the zero-velocity rows are exactly zero
     lo, hi = ref.zero_v_rows(P, 150)
     assert np.all(got[:, lo:hi, :] == 0)
