@@ -12,7 +12,10 @@
 // fresh output array -- is not read back by this thread, so the store skips the cache line fill.
 #pragma once
 #include <emmintrin.h>
+#include <sched.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <cerrno>
@@ -203,7 +206,7 @@ private:
 class Prefaulter {
 public:
     static constexpr size_t kBlock = 2u << 20;
-    Prefaulter(int threads, bool huge) : n_(threads < 1 ? 1 : threads), huge_(huge) {
+    Prefaulter(int threads, bool huge, bool numa) : n_(threads < 1 ? 1 : threads), huge_(huge), numa_(numa) {
         try {
             workers_.reserve((size_t)n_);
             for (int i = 0; i < n_; ++i) workers_.emplace_back([this] { loop(); });
@@ -218,6 +221,10 @@ public:
     // (end() was called).
     void begin(const std::vector<std::pair<void*, size_t>>& ranges) {
         blocks_.clear();
+        if (numa_) {   // the calling thread's NUMA node: the workers' faults allocate there
+            unsigned cpu = 0, node = 0;
+            node_ = syscall(SYS_getcpu, &cpu, &node, nullptr) == 0 ? (int)node : -1;
+        }
         for (const auto& r : ranges) {
             const uintptr_t a = (uintptr_t)r.first, e = a + r.second;
             if (huge_) {   // the range's whole 2 MiB extents (advice only: errors are ignored)
@@ -280,6 +287,12 @@ private:
                 if (stop_) return;
                 seen = gen_.load(std::memory_order_acquire);
             }
+            // fault the caller's pages on the caller's NUMA node (a worker may run on the other
+            // socket; remote pages cost the caller's later reads -- and, measured, their release)
+            if (numa_ && node_ >= 0 && node_ != my_node_ && node_ < 64) {
+                const unsigned long mask = 1ul << node_;
+                if (syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, &mask, 64ul + 1) == 0) my_node_ = node_;
+            }
             for (;;) {
                 if (cancel_.load(std::memory_order_acquire)) break;
                 const size_t i = next_.fetch_add(1, std::memory_order_acq_rel);
@@ -313,7 +326,10 @@ private:
     std::atomic<size_t> next_{0};
     std::atomic<bool> cancel_{false};
     std::atomic<int> active_{0};
-    bool huge_;
+    bool huge_, numa_;
+    int node_ = -1;                       // the current job's NUMA node (begin())
+    static thread_local int my_node_;     // a worker's preferred node so far
 };
+inline thread_local int Prefaulter::my_node_ = -1;
 
 }  // namespace rsp

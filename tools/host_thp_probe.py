@@ -36,6 +36,32 @@ def thp_kib(arrs):
     return hp, rss
 
 
+def numa_kib(arrs):
+    """KiB of the arrays' mappings per NUMA node (/proc/self/numa_maps N<k>= page counts)."""
+    spans = [(a.ctypes.data, a.ctypes.data + a.nbytes) for a in arrs]
+    starts = []
+    with open("/proc/self/maps") as f:
+        for line in f:
+            lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
+            if any(lo < e and b < hi for b, e in spans):
+                starts.append(lo)
+    per = {}
+    with open("/proc/self/numa_maps") as f:
+        for line in f:
+            p = line.split()
+            if int(p[0], 16) not in starts:
+                continue
+            kps = 4
+            for t in p:
+                if t.startswith("kernelpagesize_kB="):
+                    kps = int(t.split("=")[1])
+            for t in p:
+                if t.startswith("N") and "=" in t:
+                    k, v = t.split("=")
+                    per[k] = per.get(k, 0) + int(v) * kps
+    return per
+
+
 def main():
     from rsp import _capi as capi, presets, synth
     from rsp.engine import Engine
@@ -46,7 +72,11 @@ def main():
     h = np.ascontiguousarray(np.swapaxes(synth.echo_numpy(spec, n, seed=5).astype(np.complex128), 1, 2))
     V, Ro = eng.shape
     src = np.ones((n, Ro, V), np.float32)
-    out = {"thp_enabled": open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()}
+    import ctypes
+    cpu, node = ctypes.c_uint(), ctypes.c_uint()
+    ctypes.CDLL(None).syscall(309, ctypes.byref(cpu), ctypes.byref(node), None)   # SYS_getcpu (x86-64)
+    out = {"thp_enabled": open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip(),
+           "prefault_numa": os.environ.get("RSP_PREFAULT_NUMA", "1"), "caller_cpu_node": [cpu.value, node.value]}
     for mode in ("library", "numpy_fill", "untouched"):
         rows = []
         for rep in range(4):
@@ -58,9 +88,11 @@ def main():
                 o[1][...] = 1
                 o[2][...] = 1
             hp, rss = thp_kib(o)
+            nodes = numa_kib(o)
             t0 = time.perf_counter()
             del o
-            rows.append({"anon_huge_kib": hp, "rss_kib": rss, "release_ms": round((time.perf_counter() - t0) * 1e3, 3)})
+            rows.append({"anon_huge_kib": hp, "rss_kib": rss, "numa_kib": nodes,
+                         "release_ms": round((time.perf_counter() - t0) * 1e3, 3)})
         out[mode] = rows
     print(json.dumps(out))
     eng.close()
