@@ -918,12 +918,14 @@ def main():
                     k["achieved"] = round(ab / (avg_us * 1e3), 1)
                     k["frac"] = round(ab / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
                     k["frac_basis"] = "own I/O (incl. the PC->MTD scratch)"
-                # `frac_alg` (the contract's definition): the chain's algorithmic bytes
-                # per unit x the units one launch processes / the launch's average time / peak
-                upl = units / max(n, 1)
-                k["units_per_launch"] = round(upl, 3)
-                k["alg_bytes_per_launch"] = int(upl * cpi_bytes)
-                k["frac_alg"] = round(upl * cpi_bytes / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
+                    # `frac_alg` (the contract's definition): the chain's algorithmic
+                    # bytes per unit x the units one launch processes / the launch's average time /
+                    # peak -- for the two passes that carry the compulsory bytes (the range stage
+                    # reads a few cells per Doppler hit and moves none of them)
+                    upl = units / max(n, 1)
+                    k["units_per_launch"] = round(upl, 3)
+                    k["alg_bytes_per_launch"] = int(upl * cpi_bytes)
+                    k["frac_alg"] = round(upl * cpi_bytes / (avg_us * 1e3) / HBM_PEAK_GBPS, 4)
                 if pmc and name in pmc.get("kernels", {}):
                     pk = pmc["kernels"][name]
                     k["hbm_bytes_per_launch"] = pk.get("hbm_bytes_per_launch")
@@ -940,7 +942,7 @@ def main():
             dom = max(kernels, key=lambda q: kernels[q][0])
             roof["dominant_kernel"] = dom
             roof["dominant_ms_per_step"] = round(kernels[dom][0], 3)
-            roof["dominant_frac_alg"] = ks[dom]["frac_alg"]
+            roof["dominant_frac_alg"] = ks[dom].get("frac_alg")
             if "valu_frac" in ks.get(dom, {}):
                 roof["valu_frac"] = ks[dom]["valu_frac"]
                 roof["valu_frac_source"] = "profiles/pmc_%s.json (dominant kernel, SQ counters)" % tag

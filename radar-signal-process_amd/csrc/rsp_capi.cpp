@@ -1956,8 +1956,9 @@ static int host_chain_small(rsp_ctx* ctx, const void* echo, int32_t dtype, int32
 // the copy threads would otherwise take one page fault + zeroing per 4 KiB as they deliver.
 // The job ends (workers off the caller's memory) before the call returns, on every path.
 // Dev A/B: RSP_PREFAULT=0 off; RSP_PREFAULT_THREADS (default 4); RSP_PREFAULT_HUGE=0 (no
-// MADV_HUGEPAGE advice); RSP_PREFAULT_NUMA=0 (workers fault wherever they run, not on the
-// calling thread's NUMA node).
+// MADV_HUGEPAGE advice).  (Faulting on the calling thread's NUMA node was measured neutral on the
+// GPU box -- every page landed on node 0 either way, profiles/r06/host/numa_ab/ -- and is not
+// kept.)
 static constexpr size_t kPrefaultMin = 8u << 20;
 struct PrefaultJob {
     rsp_ctx* ctx = nullptr;
@@ -1972,12 +1973,11 @@ static void host_prefault(rsp_ctx* ctx, PrefaultJob& job, const std::vector<std:
     static const int mode = zc_knob("RSP_PREFAULT", 1);
     static const int nthr = zc_knob("RSP_PREFAULT_THREADS", 4);
     static const int huge = zc_knob("RSP_PREFAULT_HUGE", 1);
-    static const int numa = zc_knob("RSP_PREFAULT_NUMA", 1);
     size_t total = 0;
     for (const auto& r : ranges) total += r.first ? r.second : 0;
     if (mode == 0 || total < kPrefaultMin) return;
     auto& h = ctx->hp;
-    if (!h.prefault) h.prefault.reset(new rsp::Prefaulter(nthr, huge != 0, numa != 0));
+    if (!h.prefault) h.prefault.reset(new rsp::Prefaulter(nthr, huge != 0));
     std::vector<std::pair<void*, size_t>> rs;
     for (const auto& r : ranges)
         if (r.first && r.second) rs.push_back(r);

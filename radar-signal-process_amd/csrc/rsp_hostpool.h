@@ -12,10 +12,7 @@
 // fresh output array -- is not read back by this thread, so the store skips the cache line fill.
 #pragma once
 #include <emmintrin.h>
-#include <sched.h>
 #include <sys/mman.h>
-#include <sys/syscall.h>
-#include <unistd.h>
 
 #include <atomic>
 #include <cerrno>
@@ -201,12 +198,15 @@ private:
 // fault maps and zeroes 2 MiB.  Before the copy threads write a host range, wait() makes sure
 // its blocks are done, faulting any block no worker has claimed yet itself, so the delivery is
 // never slower than faulting in place.  Host probe (tools/micro/prefault_probe.cpp, 100 MiB of
-// fresh memory): MADV_POPULATE_WRITE 2.4-2.7 GB/s whatever the thread count; per-page touch
-// 1.6 / 4.8 / 8.2 GB/s on 1 / 4 / 8 threads; with MADV_HUGEPAGE 5.5 / 18.9 / 32 GB/s.
+// fresh memory, the GPU box): per-page touch 6.8 / 14.9 GB/s on 1 / 4 threads, with MADV_HUGEPAGE
+// 25 / 74-77 GB/s (MADV_POPULATE_WRITE: 16-38 GB/s); in this container populate does not scale
+// at all (2.4-2.7 GB/s), the touch does.  The same probe times the release: munmap of that memory
+// costs 4.6 / 7.3 / 9.0 ms on the box when 1 / 4 / 8 threads faulted it -- the caller's cost of
+// freeing new arrays, which no prefault removes.
 class Prefaulter {
 public:
     static constexpr size_t kBlock = 2u << 20;
-    Prefaulter(int threads, bool huge, bool numa) : n_(threads < 1 ? 1 : threads), huge_(huge), numa_(numa) {
+    Prefaulter(int threads, bool huge) : n_(threads < 1 ? 1 : threads), huge_(huge) {
         try {
             workers_.reserve((size_t)n_);
             for (int i = 0; i < n_; ++i) workers_.emplace_back([this] { loop(); });
@@ -221,10 +221,6 @@ public:
     // (end() was called).
     void begin(const std::vector<std::pair<void*, size_t>>& ranges) {
         blocks_.clear();
-        if (numa_) {   // the calling thread's NUMA node: the workers' faults allocate there
-            unsigned cpu = 0, node = 0;
-            node_ = syscall(SYS_getcpu, &cpu, &node, nullptr) == 0 ? (int)node : -1;
-        }
         for (const auto& r : ranges) {
             const uintptr_t a = (uintptr_t)r.first, e = a + r.second;
             if (huge_) {   // the range's whole 2 MiB extents (advice only: errors are ignored)
@@ -287,12 +283,6 @@ private:
                 if (stop_) return;
                 seen = gen_.load(std::memory_order_acquire);
             }
-            // fault the caller's pages on the caller's NUMA node (a worker may run on the other
-            // socket; remote pages cost the caller's later reads -- and, measured, their release)
-            if (numa_ && node_ >= 0 && node_ != my_node_ && node_ < 64) {
-                const unsigned long mask = 1ul << node_;
-                if (syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, &mask, 64ul + 1) == 0) my_node_ = node_;
-            }
             for (;;) {
                 if (cancel_.load(std::memory_order_acquire)) break;
                 const size_t i = next_.fetch_add(1, std::memory_order_acq_rel);
@@ -326,10 +316,7 @@ private:
     std::atomic<size_t> next_{0};
     std::atomic<bool> cancel_{false};
     std::atomic<int> active_{0};
-    bool huge_, numa_;
-    int node_ = -1;                       // the current job's NUMA node (begin())
-    static thread_local int my_node_;     // a worker's preferred node so far
+    bool huge_;
 };
-inline thread_local int Prefaulter::my_node_ = -1;
 
 }  // namespace rsp
