@@ -59,11 +59,6 @@ struct rsp_ctx {
     int64_t chunk = 0;  // 0 = default
     int nstreams = 0;   // chunk pipelines (the caller's stream + nstreams-1 internal ones); 0 = default
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
-    // (round-6 A/B experiment, RSP_FLOW2=n) the split persistent dataflow on CU-masked streams
-    hipStream_t f2_pc = nullptr, f2_mtd = nullptr;
-    hipEvent_t f2_ev[3] = {};
-    int f2_pcus = 0, f2_mcus = 0;
-    DevBuf fl_ring, fl_hring, fl_hcount, fl_ctl;
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
     // The context's scratch (PC corner turn, hit lists, internal RDM, flagV staging) is reused by
     // every _dev call: a call's stream waits for the previous call's release event first, so
@@ -316,7 +311,7 @@ int rsp_destroy(rsp_ctx* ctx) {
     for (void* p : ctx->owned) hipFree(p);
     DevBuf* bufs[] = {&ctx->pf_gain, &ctx->scratch_pc, &ctx->cat_tmp, &ctx->tmp_flagV, &ctx->tmp_rdm, &ctx->hit_list, &ctx->hit_ctr,
                       &ctx->st_in, &ctx->st_canon, &ctx->st_rdm, &ctx->st_flag, &ctx->st_flagV, &ctx->st_t,
-                      &ctx->meas_band, &ctx->ing_meta, &ctx->fl_ring, &ctx->fl_hring, &ctx->fl_hcount, &ctx->fl_ctl};
+                      &ctx->meas_band, &ctx->ing_meta};
     for (DevBuf* b : bufs)
         if (b->p) hipFree(b->p);
     for (auto& e : ctx->evs) {
@@ -1051,97 +1046,6 @@ static int range_group() {
     return g;
 }
 
-// (Round-6 A/B experiment; not the product.)  RSP_FLOW2=n: the call as the
-// split persistent dataflow -- flow2_kernel<ROLE 0> (PC units) on a stream masked to n CUs of every
-// XCD, flow2_kernel<ROLE 1> (MTD tiles + range jobs) on one masked to the other 32 - n -- for the
-// c2 / c3 shape; RSP_ERR_UNSUPPORTED otherwise (the chunked pipeline runs).
-static int flow2_cus() {
-    static const int n = [] { const char* v = getenv("RSP_FLOW2"); return v && *v ? atoi(v) : 0; }();
-    return n;
-}
-static int run_flow2(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t ncpi, const rsp::MtdArgs& m,
-                     const rsp::CfarRArgs& cr, bool cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
-                     hipStream_t s) {
-    const int64_t P = ctx->p.P, Ro = ctx->p.R_out;
-    if (!ctx->pc_v2 || ctx->pc_mf.size() != 2 || ctx->beams != 1 || ctx->V != P || m.pin != P || m.bnf > 0 ||
-        m.mti_lag > 0 || ctx->pc_mf[0].gain || ctx->pc_mf[1].gain || !d_rdm || ctx->ncat ||
-        !rsp::flow_supported((int)P, ctx->pc_mf[0].mf.nfft, ctx->pc_mf[1].mf.nfft, dtype, ctx->beams))
-        return RSP_ERR_UNSUPPORTED;
-    if (cfar && !(m.cv.ref == 5 && m.cv.save == 7 && (!cr.rflag || (cr.ref == 5 && cr.save == 7))))
-        return RSP_ERR_UNSUPPORTED;
-    if (ncpi > 0x7fffffff / 2) return RSP_ERR_UNSUPPORTED;
-    if (!ctx->f2_pc) {   // mask bit b enables one CU of XCD b % 8 (tools/micro/cumask_probe.hip)
-        int ncu = 0;
-        HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-        const int words = (ncu + 31) / 32, npc = 8 * flow2_cus();
-        if (npc <= 0 || npc >= ncu) return fail(ctx, RSP_ERR_ARG, "RSP_FLOW2=%d: %d of %d CUs", flow2_cus(), npc, ncu);
-        std::vector<uint32_t> mp((size_t)words, 0u), mm((size_t)words, 0u);
-        for (int b = 0; b < ncu; ++b) (b < npc ? mp : mm)[(size_t)(b / 32)] |= 1u << (b % 32);
-        HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->f2_pc, (uint32_t)words, mp.data()));
-        HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->f2_mtd, (uint32_t)words, mm.data()));
-        for (auto& e : ctx->f2_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ctx->f2_pcus = npc;
-        ctx->f2_mcus = ncu - npc;
-    }
-    int nreg = 0, reg = 0;
-    rsp::mtd_regions((int)P, (int)Ro, 1, &nreg, &reg, 1);   // per CPI: tiles, entries per tile
-    constexpr int64_t Q = rsp::kFlowQueues, S = rsp::kFlowSlots;
-    const int64_t Qn = ncpi < Q ? ncpi : Q;
-    const size_t plane = (size_t)P * Ro;
-    int rc;
-    if ((rc = ensure(ctx, ctx->fl_ring, (size_t)Qn * S * plane * sizeof(float2)))) return rc;
-    if ((rc = ensure(ctx, ctx->fl_ctl, (size_t)rsp::kFlowCtlLines * rsp::kFlowLine * sizeof(uint32_t)))) return rc;
-    const bool hits = cfar && cr.rflag;
-    if (hits) {
-        if ((rc = ensure(ctx, ctx->fl_hring, (size_t)Qn * S * nreg * reg * sizeof(uint32_t)))) return rc;
-        if ((rc = ensure(ctx, ctx->fl_hcount, (size_t)Qn * S * nreg * sizeof(uint32_t)))) return rc;
-    }
-    rsp::FlowArgs f;
-    std::memset(&f, 0, sizeof(f));
-    f.echo = d_echo;
-    f.a1 = ctx->pc_mf[0];
-    f.a2 = ctx->pc_mf[1];
-    f.a1.rows = f.a2.rows = (int)P;
-    f.m = m;
-    f.m.flag_zero = 1;
-    f.m.rflag = cr.rflag;
-    f.m.flag = nullptr;
-    f.m.hits = nullptr;
-    f.m.hit_count = nullptr;
-    f.m.prev_nregions = 0;
-    f.cr = cr;
-    f.ring = (float2*)ctx->fl_ring.p;
-    f.hring = hits ? (uint32_t*)ctx->fl_hring.p : nullptr;
-    f.hcount = hits ? (uint32_t*)ctx->fl_hcount.p : nullptr;
-    f.rdm = d_rdm;
-    f.flag = cfar ? d_flag : nullptr;
-    f.flagV = cfar ? d_flagV : nullptr;
-    f.ctl = (uint32_t*)ctx->fl_ctl.p;
-    f.ncpi = (int)ncpi;
-    f.lag = 2;
-    HIP_TRY(ctx, hipMemsetAsync(ctx->fl_ctl.p, 0, ctx->fl_ctl.n, s));
-    HIP_TRY(ctx, hipEventRecord(ctx->f2_ev[0], s));
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->f2_pc, ctx->f2_ev[0], 0));
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->f2_mtd, ctx->f2_ev[0], 0));
-    HIP_TRY(ctx, rsp::launch_flow2(f, dtype, ctx->f2_pc, ctx->f2_mtd, ctx->f2_pcus, ctx->f2_mcus));
-    HIP_TRY(ctx, hipEventRecord(ctx->f2_ev[1], ctx->f2_pc));
-    HIP_TRY(ctx, hipEventRecord(ctx->f2_ev[2], ctx->f2_mtd));
-    HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->f2_ev[1], 0));
-    HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->f2_ev[2], 0));
-    return RSP_OK;
-}
-// (dev) the status word of the last split-dataflow call: 1 if a bounded wait expired
-extern "C" int rsp_diag_flow2_status(rsp_ctx* ctx, int32_t* timed_out) {
-    *timed_out = 0;
-    if (!ctx->fl_ctl.p) return RSP_OK;
-    HIP_TRY(ctx, hipDeviceSynchronize());
-    uint32_t w = 0;
-    HIP_TRY(ctx, hipMemcpy(&w, (const char*)ctx->fl_ctl.p + (size_t)(rsp::kFlowCtlLines - 1) * rsp::kFlowLine * 4, 4,
-                           hipMemcpyDeviceToHost));
-    *timed_out = (int32_t)w;
-    return RSP_OK;
-}
-
 static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64_t units, int win,
                           const rsp_cfar_params* cfar, float* d_rdm, uint8_t* d_flag, uint8_t* d_flagV,
                           float* d_diff, hipStream_t s, bool pc_input) {
@@ -1154,10 +1058,6 @@ static int run_chain_body(rsp_ctx* ctx, const void* d_echo, int32_t dtype, int64
         if (rc) return rc;
     } else {
         m.cv.enabled = 0;
-    }
-    if (flow2_cus() > 0 && win == 0 && !pc_input && !d_diff) {
-        const int rc = run_flow2(ctx, d_echo, dtype, units, m, cr, cfar != nullptr, d_rdm, d_flag, d_flagV, s);
-        if (rc != RSP_ERR_UNSUPPORTED) return rc;
     }
     const int64_t ocpi = win > 0 ? win : 1;               // output CPIs per unit
     m.nwin = win;

@@ -149,39 +149,6 @@ struct MtdArgs {
 };
 
 
-// (Round-6 A/B experiment, VERDICT r5 item 1 -- not the product.)  Two persistent kernels, a
-// PC-only and an MTD-only one, on CU-masked streams: CPI c belongs to queue c % kFlowQueues (one per
-// XCD); the PC kernel's items are a queue's PC units in CPI order, the MTD kernel's its MTD tiles
-// (each carrying the range job of the queue's CPI `lag` before) and then the range-only items of
-// its last `lag` CPIs.  PC rows go through a ring of kFlowSlots scratch CPIs per queue; hand-offs
-// are write-through (sc1 stores, drained, one counter add per item) read by sc1 loads.
-constexpr int kFlowQueues = 8;
-constexpr int kFlowSlots = 4;   // >= 2 * lag
-constexpr int kFlowLine = 32;   // uint32 per control line (128 B)
-// control words: PC heads [kFlowQueues], MTD heads [kFlowQueues], counters [kFlowQueues][kFlowSlots][2]
-// (PC units, MTD tiles done), then the status line (a wait that timed out)
-constexpr int kFlowCtlLines = 2 * kFlowQueues + kFlowQueues * kFlowSlots * 2 + 1;
-struct FlowArgs {
-    const void* echo;      // [ncpi][P][R] (complex fp32 or fp16 I/Q)
-    PcMfArgs a1, a2;       // the short (FIR + MF) and the long matched-filter segment, rows = P
-    MtdArgs m;             // tile arguments (its per-launch pointers are unused)
-    CfarRArgs cr;          // range stage (cr.rflag && m.cv.enabled: range jobs run)
-    float2* ring;          // [kFlowQueues][kFlowSlots][P][R_out] PC rows
-    uint32_t* hring;       // [kFlowQueues][kFlowSlots][nm][region] Doppler hit lists
-    uint32_t* hcount;      // [kFlowQueues][kFlowSlots][nm]
-    float* rdm;            // [ncpi][V][R_out] output
-    uint8_t* flag;         // [ncpi][V][R_out] or null (no CFAR)
-    uint8_t* flagV;        // [ncpi][V][R_out] or null
-    uint32_t* ctl;         // kFlowCtlLines lines, zeroed before the launch
-    int ncpi;
-    int nl, nsh, nm;       // per CPI: long-row units, short-row groups, MTD tiles
-    int region;            // hit-list entries per tile
-    int lag;               // the MTD tiles of CPI j carry the range jobs of CPI j - lag
-};
-bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams);
-// grids of resident workgroups: pc_grid / mtd_grid (0 = resident per CU x the CU counts given)
-hipError_t launch_flow2(FlowArgs& a, int dtype, hipStream_t s_pc, hipStream_t s_mtd, int pc_cus, int mtd_cus);
-
 // Raw-data ingest (rsp_ingest.hip): one frame of uniform DDC PRT records.
 // motionParaMeasure.m's scalar arguments (rsp_measure_params, rsp_measure.hip).
 struct MeasureArgs {

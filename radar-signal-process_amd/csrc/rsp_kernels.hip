@@ -1676,242 +1676,10 @@ hipError_t launch_mtd(const float2* pc, float* rdm, uint8_t* flagV, int ncpi, co
 
 // (Round 5's persistent one-launch PC -> MTD dataflow, flow_kernel / rsp_set_flow, measured 82 %
 // of the chunked chain at c3 and left the product in round 6: DESIGN.md §7c / §7d; its source is
-// in the history, commit e3a7a73.  The sc1 (LA / SA) and opaque-index (OPQ) variants of the tile
-// and range-job templates above are what it instantiated.)
-
-// ================================================================== (round-6 A/B) split dataflow
-// a PC-only and an MTD-only persistent kernel, each on its own CU-masked stream
-// (disjoint CUs of every XCD: tools/micro/cumask_probe.hip showed both grids co-resident), so a
-// spin-wait of one kernel never holds a CU the other needs.  FlowArgs (rsp_internal.h).  Per
-// queue q (CPI c -> q = c % 8; workgroups serve the queue of their own XCD, then steal):
-//   PC item k        CPI j = k / npc, unit k % npc; waits until MTD(j - S) released its slot
-//   MTD item k < J*nm  CPI j = k / nm, tile k % nm; waits for PC(j) (all units) and, for its range
-//                    job of CPI j - D, MTD(j - D); then range-only items of the last D CPIs
-// Items of a role are claimed in order by running workgroups, every wait points to an earlier item
-// of the other role (or of the same role, D CPIs back), both grids are resident, so the smallest
-// unfinished item can always run.  Hand-offs as round 5's flow_kernel: sc1 stores, every storing
-// wave drains vmcnt before its workgroup's one counter add, sc1 loads after the counter; waits
-// bounded (0.5 s, then the status word; no later wait blocks).
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
-    return v & (uint32_t)(kFlowQueues - 1);
-}
-__device__ __forceinline__ uint32_t* flow_head(uint32_t* ctl, int role, int q) { return ctl + (role * kFlowQueues + q) * kFlowLine; }
-__device__ __forceinline__ uint32_t* flow_ctr(uint32_t* ctl, int q, int slot, int k) {
-    return ctl + (2 * kFlowQueues + (q * kFlowSlots + slot) * 2 + k) * kFlowLine;
-}
-__device__ __forceinline__ uint32_t* flow_status(uint32_t* ctl) { return ctl + (kFlowCtlLines - 1) * kFlowLine; }
-
-// thread 0: wait until *p >= target (relaxed sc1 polls, s_sleep between)
-__device__ __forceinline__ void flow_wait(uint32_t* p, uint32_t target, uint32_t* st) {
-    if (ld_u32<kSc1>(p) >= target) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (ld_u32<kSc1>(p) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (ld_u32<kSc1>(st) != 0u) return;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s of the 100 MHz clock
-            __hip_atomic_fetch_or((gu32*)st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-    }
-}
-__device__ __forceinline__ int flow_cpis(int ncpi, int q) {
-    return ncpi > q ? (ncpi - q + kFlowQueues - 1) / kFlowQueues : 0;
-}
-
-// role 0: PC units; role 1: MTD tiles + range-only items.  Returns the counter the item publishes.
-template <typename TIn, int N1, int N2, int P, int REF, int ROLE>
-__device__ __forceinline__ uint32_t* flow2_item(const FlowArgs& a, int q, uint32_t k, int nh, unsigned char* smem,
-                                                uint32_t* s_hits) {
-    using PC = PairCfg<N1, N2>;
-    constexpr int S = kFlowSlots;
-    uint32_t* st = flow_status(a.ctl);
-    const size_t R = (size_t)a.a2.R, Ro = (size_t)a.a2.R_out;
-    const size_t plane = (size_t)P * Ro;
-    const int npc = a.nl + a.nsh;
-    if constexpr (ROLE == 0) {
-        const int j = (int)(k / (uint32_t)npc), u = (int)(k % (uint32_t)npc);
-        const int c = q + kFlowQueues * j, slot = j % S;
-        const uint32_t gen = (uint32_t)(j / S);
-        if (threadIdx.x == 0 && j >= S) flow_wait(flow_ctr(a.ctl, q, slot, 1), gen * (uint32_t)a.nm, st);
-        __syncthreads();
-        const TIn* ein = (const TIn*)a.echo + (size_t)c * P * R;
-        float2* pcs = a.ring + (size_t)(q * S + slot) * P * Ro;
-        float2* lds = reinterpret_cast<float2*>(smem);
-        if (u < a.nl) {
-            constexpr int G = PcCfg<N2>::G;
-            const int ns = a.a2.nsub > 1 ? a.a2.nsub : 1;
-            pc_row<TIn, N2, G, kSc1, G == 64>(ein, pcs, a.a2, u / ns, tid_of<true>() % G, lds, u % ns);
-        } else {
-            constexpr int G = PcCfg<N1>::G;
-            const int tx = tid_of<true>();
-            const int grp = tx / G, ns = a.a1.nsub > 1 ? a.a1.nsub : 1;
-            const int uu = (u - a.nl) * PC::RPB1 + grp;
-            pc_row<TIn, N1, G, kSc1, G == 64>(ein, pcs, a.a1, uu / ns, tx % G, lds + grp * PcCfg<N1>::SLOT, uu % ns);
-        }
-        return flow_ctr(a.ctl, q, slot, 0);
-    } else {
-        const int J = flow_cpis(a.ncpi, q), D = a.lag;
-        const bool hits_on = nh > 0;
-        auto src_of = [&](int jj) {   // the range stage's view of CPI jj of this queue
-            const int ss = jj % S;
-            const size_t cc = (size_t)(q + kFlowQueues * jj);
-            return RangeSrc{a.rdm + cc * plane, a.flag ? a.flag + cc * plane : nullptr,
-                            a.hring + (size_t)(q * S + ss) * a.nm * a.region, a.hcount + (size_t)(q * S + ss) * a.nm,
-                            a.region, a.cr};
-        };
-        if (k < (uint32_t)J * (uint32_t)a.nm) {   // one MTD tile (+ Doppler CFAR, hit list) + the range job of CPI j-D
-            const int j = (int)(k / (uint32_t)a.nm), t = (int)(k % (uint32_t)a.nm);
-            const int c = q + kFlowQueues * j, slot = j % S;
-            const uint32_t gen = (uint32_t)(j / S);
-            if (threadIdx.x == 0) {
-                flow_wait(flow_ctr(a.ctl, q, slot, 0), (gen + 1) * (uint32_t)npc, st);
-                if (hits_on && j >= D) flow_wait(flow_ctr(a.ctl, q, (j - D) % S, 1), (uint32_t)((j - D) / S + 1) * a.nm, st);
-            }
-            __syncthreads();
-            MtdTile T;
-            T.pc = a.ring + (size_t)(q * S + slot) * P * Ro;
-            T.rdm = a.rdm + (size_t)c * plane;
-            T.diff = nullptr;
-            T.flagV = a.flagV ? a.flagV + (size_t)c * plane : nullptr;
-            T.flag = a.flag ? a.flag + (size_t)c * plane : nullptr;
-            T.hits = hits_on ? a.hring + ((size_t)(q * S + slot) * a.nm + t) * a.region : nullptr;
-            T.hit_count = hits_on ? a.hcount + (size_t)(q * S + slot) * a.nm + t : nullptr;
-            T.cell_base = 0;
-            T.bx = t;
-            const RangeSrc rs = src_of(j >= D ? j - D : j);
-            RangeJob57T<kSc1> rj;
-            const bool job = hits_on && j >= D;
-            if (job) rj.fetch_idx(rs, t);
-            mtd_tile<P, REF, 1, kSc1, kSc1, RangeHookT<kSc1>, true>(T, a.m, smem, s_hits, RangeHookT<kSc1>{rj, rs});
-            if (job) {
-                rj.finish(rs);
-                if (rj.n > blockDim.x)
-                    cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, t, a.region, a.cr,
-                                                (int)(threadIdx.x + blockDim.x), (int)blockDim.x);
-            }
-            return flow_ctr(a.ctl, q, slot, 1);
-        }
-        // the last D CPIs' range stage: one hit region each
-        const uint32_t kk = k - (uint32_t)J * (uint32_t)a.nm;
-        const int Dl = J < D ? J : D;   // (a queue of fewer than D CPIs carried no job at all)
-        const int j = J - Dl + (int)(kk / (uint32_t)nh), rg = (int)(kk % (uint32_t)nh);
-        if (threadIdx.x == 0) flow_wait(flow_ctr(a.ctl, q, j % S, 1), (uint32_t)(j / S + 1) * a.nm, st);
-        __syncthreads();
-        const RangeSrc rs = src_of(j);
-        cfar_hit_region<5, 7, kSc1>(rs.rdm, rs.flag, rs.hits, rs.count, rg, a.region, a.cr, (int)threadIdx.x,
-                                    (int)blockDim.x);
-        return nullptr;
-    }
-}
-
-template <int ROLE>
-__device__ __forceinline__ uint32_t flow2_total(const FlowArgs& a, int q, int nh) {
-    const int J = flow_cpis(a.ncpi, q);
-    if (J <= 0) return 0u;
-    if constexpr (ROLE == 0) return (uint32_t)J * (uint32_t)(a.nl + a.nsh);
-    const int D = J < a.lag ? J : a.lag;
-    return (uint32_t)J * (uint32_t)a.nm + (nh ? (uint32_t)D * (uint32_t)nh : 0u);
-}
-
-// One role's persistent kernel.  Per item: thread 0 waits for the item's inputs, barrier, body,
-// thread 0 claims the next item, every wave drains its stores, barrier, thread 0 publishes the
-// item and the next item number, barrier.  Every thread-0 region is fenced by barriers (a block
-// holding a barrier is never duplicated, so jump threading cannot join two thread-0 regions
-// across the back edge: round 5's hand-off probe hang).
-template <typename TIn, int N1, int N2, int P, int REF, int ROLE>
-__global__ __launch_bounds__(kBlock, 4) void flow2_kernel(FlowArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t s_item, s_hits;
-    const int nh = (a.flag && a.cr.rflag && a.m.cv.enabled) ? a.nm : 0;
-    int h = (int)xcc_id();
-    if (threadIdx.x == 0)
-        s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, ROLE, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-    int tried = 1;
-    for (;;) {
-        if (k >= flow2_total<ROLE>(a, h, nh)) {   // this queue is drained: help the next one
-            if (tried == kFlowQueues) break;
-            ++tried;
-            h = (h + 1) % kFlowQueues;
-            __syncthreads();   // every thread has read s_item
-            if (threadIdx.x == 0)
-                s_item = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, ROLE, h), 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-            continue;
-        }
-        // the arguments through an opaque copy of the kernarg pointer (round 5: otherwise hipcc
-        // hoists every field into SGPRs for the whole loop and spills)
-        typedef const __attribute__((address_space(4))) FlowArgs FlowArgsK;
-        const FlowArgsK* ap = (const FlowArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ap));
-        const FlowArgs& ai = *(const FlowArgs*)ap;
-        uint32_t* sig = flow2_item<TIn, N1, N2, P, REF, ROLE>(ai, h, k, nh, smem, &s_hits);
-        uint32_t nxt = 0;
-        if (threadIdx.x == 0)
-            nxt = __hip_atomic_fetch_add((gu32*)flow_head(a.ctl, ROLE, h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done (sc1: in memory)
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if (sig) __hip_atomic_fetch_add((gu32*)sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_item = nxt;
-        }
-        __syncthreads();
-        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-    }
-}
-
-template <typename TIn, int N1, int N2, int P, int REF>
-static hipError_t launch_flow2_t(FlowArgs& a, hipStream_t s_pc, hipStream_t s_mtd, int pc_cus, int mtd_cus) {
-    using PC = PairCfg<N1, N2>;
-    using MC = MtdCfg<P>;
-    static_assert(PC::T == kBlock && MC::T == kBlock, "flow items are 256-thread workgroups");
-    constexpr size_t lpc = PC::lds, lmtd = MC::template lds_for<REF>();
-    static LaunchOnce o0, o1;
-    int per0 = 0, per1 = 0;
-    hipError_t e = launch_once(o0, &per0, [&](int, int* v) {
-        hipError_t r = hipFuncSetAttribute((const void*)flow2_kernel<TIn, N1, N2, P, REF, 0>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lpc);
-        if (r != hipSuccess) return r;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(v, (const void*)flow2_kernel<TIn, N1, N2, P, REF, 0>, kBlock, lpc);
-    });
-    if (e != hipSuccess) return e;
-    e = launch_once(o1, &per1, [&](int, int* v) {
-        hipError_t r = hipFuncSetAttribute((const void*)flow2_kernel<TIn, N1, N2, P, REF, 1>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lmtd);
-        if (r != hipSuccess) return r;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(v, (const void*)flow2_kernel<TIn, N1, N2, P, REF, 1>, kBlock, lmtd);
-    });
-    if (e != hipSuccess) return e;
-    if (per0 < 1 || per1 < 1) return hipErrorLaunchOutOfResources;
-    const int ns2 = a.a2.nsub > 1 ? a.a2.nsub : 1, ns1 = a.a1.nsub > 1 ? a.a1.nsub : 1;
-    a.nl = P * ns2;
-    a.nsh = (P * ns1 + PC::RPB1 - 1) / PC::RPB1;
-    a.nm = (a.a2.R_out + MC::W - 1) / MC::W;
-    a.region = MC::W * P;
-    hipLaunchKernelGGL((flow2_kernel<TIn, N1, N2, P, REF, 0>), dim3((unsigned)(per0 * pc_cus)), dim3(kBlock), lpc, s_pc, a);
-    hipError_t r = hipGetLastError();
-    if (r != hipSuccess) return r;
-    hipLaunchKernelGGL((flow2_kernel<TIn, N1, N2, P, REF, 1>), dim3((unsigned)(per1 * mtd_cus)), dim3(kBlock), lmtd, s_mtd, a);
-    return hipGetLastError();
-}
-
-bool flow_supported(int P, int nfft1, int nfft2, int dtype, int beams) {
-    return beams == 1 && P == 128 && nfft1 == 1024 && nfft2 == 4096 && (dtype == RSP_C64 || dtype == RSP_C32F16);
-}
-
-hipError_t launch_flow2(FlowArgs& a, int dtype, hipStream_t s_pc, hipStream_t s_mtd, int pc_cus, int mtd_cus) {
-    if (a.ncpi <= 0) return hipSuccess;
-    if (!flow_supported(a.m.P, a.a1.mf.nfft, a.a2.mf.nfft, dtype, a.m.beams)) return hipErrorNotSupported;
-    if (a.m.cv.enabled && !(a.m.cv.ref == 5 && a.m.cv.save == 7)) return hipErrorNotSupported;
-    if (a.m.cv.enabled && a.cr.rflag && !(a.cr.ref == 5 && a.cr.save == 7)) return hipErrorNotSupported;
-    if (dtype == RSP_C64) return launch_flow2_t<float2, 1024, 4096, 128, 5>(a, s_pc, s_mtd, pc_cus, mtd_cus);
-    return launch_flow2_t<__half2, 1024, 4096, 128, 5>(a, s_pc, s_mtd, pc_cus, mtd_cus);
-}
+// in the history, commit e3a7a73.  Round 6's split form -- a PC-only and an MTD-only persistent
+// kernel on CU-masked streams -- measured 75.6 % (profiles/r06/flow2/ab_record.txt, commit
+// d7d9bbe).  The sc1 (LA / SA) and opaque-index (OPQ) variants of the tile and range-job templates
+// above are what they instantiated.)
 
 // ================================================================== Doppler CFAR from an RDM
 // rsp_cfar's first stage: tile of W columns x V rows staged column-major in LDS.
