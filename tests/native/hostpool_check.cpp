@@ -2,11 +2,14 @@
 // tests/test_hostpool.py: every conversion against a scalar loop, over thread counts, sizes
 // either side of the split threshold and misaligned destinations, with many back-to-back jobs
 // (the spin / block hand-off) -- exit 0 and "ok" on success.
+#include <sys/mman.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "rsp_hostpool.h"
@@ -67,6 +70,54 @@ int main(int argc, char** argv) {
                     CHECK(ok, "widen_u8 t%d n%zu off%d", threads, n, off);
                     pool.copy(f.data() + off, fsrc.data(), n * 4);
                     CHECK(std::memcmp(f.data() + off, fsrc.data(), n * 4) == 0, "copy t%d n%zu off%d", threads, n, off);
+                }
+            }
+        }
+    }
+    // rsp::Prefaulter (the host calls' output prefault): fresh anonymous ranges at unaligned
+    // offsets, some bytes written before the job (their contents must survive the faulting), two
+    // copier threads that wait() per piece and then write it, and jobs abandoned early (end()
+    // before every block was waited for).  Every byte ends as the copier or the early writer left it.
+    for (int threads : {1, 4}) {
+        for (bool huge : {false, true}) {
+            rsp::Prefaulter pf(threads, huge);
+            for (int job = 0; job < (rounds > 4 ? 12 : 4); ++job) {
+                const size_t sizes[3] = {(size_t)(5u << 20) + 4097u, (size_t)(1u << 20) + 13u, (size_t)(3u << 20) + 1u};
+                char* maps[3];
+                char* base[3];
+                std::vector<std::pair<void*, size_t>> ranges;
+                for (int r = 0; r < 3; ++r) {
+                    maps[r] = (char*)mmap(nullptr, sizes[r] + 8192, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+                    CHECK(maps[r] != MAP_FAILED, "mmap");
+                    base[r] = maps[r] + 8 + 512 * r + job;   // unaligned starts
+                    // an early writer: every 7th page's first bytes before the job begins
+                    for (size_t o = 0; o < sizes[r]; o += 7 * 4096) base[r][o] = (char)(0x5a + r);
+                    ranges.push_back({base[r], sizes[r]});
+                }
+                const bool abandon = job % 3 == 2;
+                pf.begin(ranges);
+                auto copier = [&](int r) {
+                    const size_t piece = 700000 + 1000 * (size_t)r;
+                    const size_t lim = abandon ? sizes[r] / 3 : sizes[r];
+                    for (size_t o = 0; o < lim; o += piece) {
+                        const size_t n = lim - o < piece ? lim - o : piece;
+                        pf.wait(base[r] + o, n);
+                        std::memset(base[r] + o, (char)(r + 1), n);
+                    }
+                };
+                std::thread t0([&] { copier(0); copier(2); });
+                std::thread t1([&] { copier(1); });
+                t0.join();
+                t1.join();
+                pf.end();
+                for (int r = 0; r < 3; ++r) {
+                    const size_t lim = abandon ? sizes[r] / 3 : sizes[r];
+                    bool ok = true;
+                    for (size_t o = 0; o < sizes[r] && ok; o += 997)
+                        ok = o < lim ? base[r][o] == (char)(r + 1)
+                                     : (base[r][o] == ((o % (7 * 4096)) == 0 ? (char)(0x5a + r) : (char)0));
+                    CHECK(ok, "prefault t%d huge%d job%d range%d", threads, (int)huge, job, r);
+                    munmap(maps[r], sizes[r] + 8192);
                 }
             }
         }

@@ -1,7 +1,9 @@
 """The host copy pool of the host-buffer path (radar-signal-process_amd/csrc/rsp_hostpool.h:
-spin-then-block job hand-off, streaming-store conversions) on the CPU: every conversion equals
-the scalar cast over thread counts, split sizes and misaligned destinations, and a
-ThreadSanitizer build of the same check reports no race (when the toolchain has TSan)."""
+spin-then-block job hand-off, streaming-store conversions) and the output prefault (Prefaulter:
+helper threads faulting the caller's fresh output ranges, per-block waits, abandoned jobs) on the
+CPU: every conversion equals the scalar cast over thread counts, split sizes and misaligned
+destinations, every byte of a prefaulted range ends as its writers left it, and a ThreadSanitizer
+build of the same check reports no race (when the toolchain has TSan)."""
 import os
 import subprocess
 
