@@ -279,3 +279,39 @@ def test_cfar_f64_dma_fallback_matches_cfar(torch_cuda):
         assert np.array_equal(f64, f8.astype(np.float64)) and np.array_equal(v64, v8.astype(np.float64))
         assert v8.sum() > 0
     eng.close()
+
+
+@pytest.mark.parametrize("out_layout,f64", [(0, False), (1, False), (1, True)])
+def test_prefaulted_new_outputs_equal_device_path(torch_cuda, out_layout, f64):
+    """Host calls whose outputs total >= 8 MiB fault the caller's new output arrays in ahead of
+    the copies (rsp_hostpool.h Prefaulter, 2 MiB blocks, huge-page advice): 24 CPIs of 64 x 1024
+    (9.4 MiB of float / byte outputs, 25 MiB as doubles) through the chunked DMA pipeline, into
+    fresh arrays and into reused arrays pre-filled with garbage, both layouts and the double
+    outputs -- all bit-exact against the device path, call after call."""
+    torch = torch_cuda
+    import ctypes as C
+    from rsp import _capi as capi
+    from rsp import presets, synth
+    eng = _engine(64, 1024)
+    cf = presets.default_cfar(eng.spec)
+    cp = cf.to_c()
+    V, Ro = eng.shape
+    B = 24
+    lib = eng.lib
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    echo = synth.echo_numpy(eng.spec, B, seed=2024).astype(np.complex64)
+    want = _dev(torch, eng, echo, cf)
+    if out_layout == capi.RSP_COLMAJOR:
+        want = tuple(np.ascontiguousarray(np.swapaxes(w, 1, 2)) for w in want)
+    col = np.ascontiguousarray(np.swapaxes(echo.astype(np.complex128), 1, 2))
+    oshape = want[0].shape
+    dt = (np.float64, np.float64) if f64 else (np.float32, np.uint8)
+    reused = (np.full(oshape, 3.0, dt[0]), np.full(oshape, 9, dt[1]), np.full(oshape, 9, dt[1]))
+    for call in range(3):
+        for outs in ((np.empty(oshape, dt[0]), np.empty(oshape, dt[1]), np.empty(oshape, dt[1])), reused):
+            fn = lib.rsp_pc_mtd_cfar_f64 if f64 else lib.rsp_pc_mtd_cfar
+            assert fn(eng.ctx, ptr(col), capi.RSP_C128, capi.RSP_COLMAJOR, 64, 1024, B, C.byref(cp), ptr(outs[0]),
+                      out_layout, ptr(outs[1]), ptr(outs[2])) == 0
+            for g, w in zip(outs, want):
+                assert np.array_equal(g, w.astype(g.dtype)), call
+    eng.close()

@@ -249,3 +249,40 @@ def test_bluestein_mtd_parity(torch_cuda, P, R, batch):
     assert soft <= 2 and softv <= 2
     assert flagV.sum() > 0
     eng.close()
+
+
+def test_window_stream_with_range_concat(torch_cuda):
+    """The sliding-window stream (rsp_window_pc_mtd_cfar_dev) on a context with main.m's range
+    concatenation (rsp_set_range_concat): each frame's PC is computed once at the full 1031
+    columns, gathered to 868, and every window reads its rows from the gathered frame -- bit-exact
+    against the chain on the explicitly sliced windows of the same context."""
+    torch = torch_cuda
+    from rsp import presets
+    from rsp.engine import Engine
+    spec = presets.legacy(64, 1031, concat=True)
+    cf = presets.default_cfar(spec)
+    eng = Engine(spec)
+    F, win, P = 3, 4, 64
+    from rsp import synth
+    frames = synth.echo_torch(spec, F + 1, seed=77).reshape(1, F + 1, P, 1031)
+    rdm = torch.empty((1, F, win, P, 868), dtype=torch.float32, device="cuda")
+    flag = torch.empty((1, F, win, P, 868), dtype=torch.uint8, device="cuda")
+    eng.window_dev(frames, win, rdm=rdm, flag=flag, cfar=cf)
+    torch.cuda.synchronize()
+    for n in range(F):
+        pair = torch.cat([frames[0, n], frames[0, n + 1]], dim=0)
+        wins = torch.stack([pair[_mround(i * P / win):_mround(i * P / win) + P] for i in range(win)]).contiguous()
+        r2 = torch.empty((win, P, 868), dtype=torch.float32, device="cuda")
+        f2 = torch.empty((win, P, 868), dtype=torch.uint8, device="cuda")
+        eng.run_dev(wins, rdm=r2, flag=f2, cfar=cf)
+        torch.cuda.synchronize()
+        assert torch.equal(r2, rdm[0, n]) and torch.equal(f2, flag[0, n]), n
+    # one frame pair per chunk on two pipelines: each pipeline gathers from its own full-width slot
+    eng.set_chunk(win)
+    eng.set_streams(2)
+    r3 = torch.empty_like(rdm)
+    f3 = torch.empty_like(flag)
+    eng.window_dev(frames, win, rdm=r3, flag=f3, cfar=cf)
+    torch.cuda.synchronize()
+    assert torch.equal(r3, rdm) and torch.equal(f3, flag)
+    eng.close()
