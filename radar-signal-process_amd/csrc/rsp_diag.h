@@ -10,9 +10,6 @@
 //   -DRSP_DIAG_PC_WAVES=n      minimum waves per SIMD of the PC kernel (__launch_bounds__)
 //   -DRSP_DIAG_PC_LDS_EXTRA=b  extra dynamic LDS per PC workgroup (caps workgroups per CU)
 //   -DRSP_MTD_NO_DMA           MTD tile loads to registers instead of LDS-DMA (the round-3 form)
-//   -DRSP_PC_DMA=1             PC long rows by LDS-DMA into the exchange slot (round-4 A/B, not the
-//                              product; the rejected persistent 2-slot ring variant is in the
-//                              history, commit f50fb2c, not in this file)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -278,44 +278,10 @@ __device__ __forceinline__ void fir_row(const TIn* __restrict__ x, float2* __res
     xsync<WS>();
 }
 
-// Row input by LDS-DMA (dev-only -DRSP_PC_DMA, A/B of VERDICT r3 item 1): a long row's N input
-// samples go global -> its LDS exchange slot by `buffer_load_dwordx4 ... lds` (16 B per lane, 1 KiB
-// contiguous per wave instruction, no VGPR destination), then each thread reads its strided
-// elements u[m] = x[t + G*m] from the slot (lane-contiguous ds_read_b64: conflict-free).  The
-// buffer range check supplies the zero padding past in_len; it is per dword on gfx950, also for
-// LDS-DMA (tools/micro/lds_dma_probe.hip), so a 16-byte piece that straddles in_len keeps its
-// in-range elements.
-template <int N, int G, typename TIn>
-__host__ __device__ constexpr bool kDmaIn() {
-#if defined(RSP_PC_DMA) && RSP_PC_DMA == 1
-    return G >= 256 && G % 64 == 0 && (N * (int)sizeof(TIn)) % (G * 16) == 0;
-#else
-    return false;
-#endif
-}
-typedef __attribute__((address_space(3))) void lds_void;
-
-template <typename TIn, int N, int G>
-__device__ __forceinline__ void pc_dma_issue(const TIn* x, uint32_t nbytes, float2* slot, int t) {
-    constexpr int NQ = N * (int)sizeof(TIn) / (G * 16);
-    const auto xr = buf_rsrc(x, nbytes);
-    const int wb = __builtin_amdgcn_readfirstlane(t & ~63);
-    char* l = reinterpret_cast<char*>(slot);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(l + (q * G + wb) * 16), 16, (uint32_t)(q * G + t) * 16u,
-                                                  0, 0, 0);
-}
-
-template <typename TIn, int N, int G>
-__device__ __forceinline__ void pc_dma_read(float2 (&u)[N / G], float2* slot, int t) {
-    constexpr int E = N / G;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const TIn* l = reinterpret_cast<const TIn*>(slot);
-#pragma unroll
-    for (int m = 0; m < E; ++m) u[m] = ld_c(l + t + G * m);
-}
+// (The long rows' input by LDS-DMA into the exchange slot, round 4's `-DRSP_PC_DMA` A/B, measured
+// +0..1 % at c3 and -1.4 % at c5 and is not kept: DESIGN.md §7b; the source is in the history,
+// commit e3a7a73.)
+typedef __attribute__((address_space(3))) void lds_void;   // an LDS-DMA destination (the MTD tiles)
 
 // One row's matched-filter segment (and optionally its FIR segment) by G threads.
 // G >= 64: a row spans whole waves, so the row index is wave-uniform (readfirstlane makes
@@ -368,9 +334,7 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
     constexpr int NW = tw_regs<N, E>() > 0 ? tw_regs<N, E>() : 1;
     float2 w[NW];
     tw_preload<N, G, 1, E, 0, NW>(w, t, tw);
-    if constexpr (kDmaIn<N, G, TIn>()) {
-        pc_dma_issue<TIn, N, G>(x + in_start, valid ? (uint32_t)in_len * ES : 0u, buf, t);
-    } else if constexpr (kUniform) {
+    if constexpr (kUniform) {
         const auto xr = buf_rsrc(x + in_start, valid ? (uint32_t)in_len * ES : 0u);
 #pragma unroll
         for (int m = 0; m < E; ++m) u[m] = buf_ld_c((const TIn*)nullptr, xr, (uint32_t)e0 * ES, (uint32_t)(G * m) * ES);
@@ -388,15 +352,11 @@ __device__ __forceinline__ void pc_row(const TIn* __restrict__ echo, float2* __r
             for (int m = 0; m < E; ++m) u[m] = cscale(u[m], buf_ld_f(gr, (uint32_t)e0 * 4u, (uint32_t)(G * m) * 4u));
         }
     };
-    if constexpr (!kDmaIn<N, G, TIn>()) apply_gain();
+    apply_gain();
     float2 hs[kEarly ? E : 1];
     if constexpr (kEarly) {
 #pragma unroll
         for (int m = 0; m < E; ++m) hs[m] = buf_ld_f2(hr, (uint32_t)e0 * 8u, (uint32_t)(G * m) * 8u);
-    }
-    if constexpr (kDmaIn<N, G, TIn>()) {   // the row has landed in the slot: to registers
-        pc_dma_read<TIn, N, G>(u, buf, t);
-        apply_gain();
     }
     // the FIR segment's staging loads ride on the same memory round trip (a second, dependent
     // round trip made the short rows' FIR phase ~40 % of their lifetime: tools/diag_stamps.py)
