@@ -245,3 +245,25 @@ def test_range_concate_restatement():
     assert np.array_equal(c[:, 318], s[:, 481]) and np.array_equal(c[:, 867], s[:, 1030])
     spec = presets.legacy(48, 1031, concat=True)
     assert spec.R_out == 868 and spec.pc_width == 1031 and spec.cfar_segments == [(0, 82), (82, 318), (318, 868)]
+
+
+def test_pc_and_mtd_restatements_against_direct_sums():
+    """Oracle-independent forms of the two transforms (no FFT on the checking side):
+    fun_pulse_compression (MTD/fun_pulse_compression.m:10-39, y = ifft(fft(x,N).*fft(h,N)) with
+    h = conj(fliplr(s0)), N = len(x)+len(h)-1) against the direct linear convolution; the segment
+    cut of fun_lss_pulse_compression (out[n] = y[len(s0)-1+n] = sum_k x[n+k] conj(s0[k])) against
+    that correlation sum; and fun_Process_MTD (fun_Process_MTD.m:27-37, |fftshift(fft(col.*kaiser))|)
+    against a P x P DFT matrix, the shift as a roll by floor(P/2)."""
+    rng = np.random.default_rng(17)
+    s0 = rng.standard_normal(37) + 1j * rng.standard_normal(37)
+    x = rng.standard_normal(211) + 1j * rng.standard_normal(211)
+    y = ref.fun_pulse_compression(s0, x)
+    np.testing.assert_allclose(y, np.convolve(x, np.conj(s0[::-1])), rtol=0, atol=1e-11 * np.abs(y).max())
+    corr = np.array([np.sum(x[n:n + len(s0)] * np.conj(s0[:len(x[n:n + len(s0)])])) for n in range(len(x))])
+    np.testing.assert_allclose(y[len(s0) - 1:len(s0) - 1 + len(x)], corr, rtol=0, atol=1e-11 * np.abs(y).max())
+    for P in (16, 48, 128):
+        pc = rng.standard_normal((P, 9)) + 1j * rng.standard_normal((P, 9))
+        k = np.arange(P)
+        dft = np.exp(-2j * np.pi * np.outer(k, k) / P)
+        want = np.abs(np.roll(dft @ (pc * ref.kaiser(P, 8.0)[:, None]), P // 2, axis=0))
+        np.testing.assert_allclose(ref.fun_Process_MTD(pc), want, rtol=0, atol=1e-11 * want.max())
