@@ -11,6 +11,9 @@
  *   - rsp_cfar_f64 on the double RDM (executeCFAR): the chain's flags;
  *   - the target: the RDM maximum lies on Doppler row FD + P/2 (the fftshift) and range column
  *     TGT (the matched filter's peak at the echo's first sample), and the CFAR flags it;
+ *   - rsp_set_range_concat (fun_lss_range_concate): the RDM of two concatenated column ranges is
+ *     the full RDM's columns gathered, bit for bit; a part past the width is RSP_ERR_ARG; 0 parts
+ *     restore the full width;
  *   - the error contract: a wrong shape is RSP_ERR_SHAPE with a message, a null context
  *     RSP_ERR_ARG.
  * Prints "ok <peak row> <peak column> <detections>" and exits 0, or prints the failed check
@@ -126,6 +129,32 @@ int main(void) {
     for (int dr = -1; dr <= 1; ++dr)
         if (br + dr >= 0 && br + dr < R && fl[(size_t)bv * R + br + dr]) flagged = 1;
     CHECK(flagged, "the CFAR does not flag the target (row %d, column %d)", bv, br);
+    /* range concatenation (fun_lss_range_concate): the MTD transforms each range column on its
+     * own, so the concatenated RDM is the full RDM's columns gathered, bit for bit -- the second
+     * part holds the target */
+    {
+        const int64_t cs[2] = {3000, 1000}, cl[2] = {600, 1200}, W = 1800;
+        float* rdm_k = malloc((size_t)P * W * 4);
+        rc = rsp_set_range_concat(ctx, 2, cs, cl);
+        CHECK(rc == RSP_OK, "rsp_set_range_concat: %d %s", rc, rsp_last_error(ctx));
+        rc = rsp_pc_mtd(ctx, row, RSP_C128, RSP_ROWMAJOR, P, R, 1, rdm_k, RSP_ROWMAJOR);
+        CHECK(rc == RSP_OK, "rsp_pc_mtd after concat: %d %s", rc, rsp_last_error(ctx));
+        same = rc == RSP_OK;
+        for (int v = 0; v < P && same; ++v)
+            for (int64_t j = 0; j < W; ++j) {
+                const int64_t src = j < cl[0] ? cs[0] + j : cs[1] + j - cl[0];
+                if (rdm_k[(size_t)v * W + j] != rdm[(size_t)v * R + src]) { same = 0; break; }
+            }
+        CHECK(same, "the concatenated RDM is not the full RDM's gathered columns");
+        const int64_t bs[1] = {R - 10}, bl[1] = {20};
+        rc = rsp_set_range_concat(ctx, 1, bs, bl);
+        CHECK(rc == RSP_ERR_ARG && strlen(rsp_last_error(ctx)) > 0, "a part past the PC width: status %d", rc);
+        rc = rsp_set_range_concat(ctx, 0, NULL, NULL);
+        CHECK(rc == RSP_OK, "rsp_set_range_concat(0 parts): %d", rc);
+        rc = rsp_pc_mtd(ctx, row, RSP_C128, RSP_ROWMAJOR, P, R, 1, rdm2, RSP_ROWMAJOR);
+        CHECK(rc == RSP_OK && memcmp(rdm2, rdm, n * 4) == 0, "the full width is not restored (%d)", rc);
+        free(rdm_k);
+    }
     /* error contract */
     rc = rsp_pc_mtd_cfar(ctx, row, RSP_C128, RSP_ROWMAJOR, P + 1, R, 1, &cf, rdm, RSP_ROWMAJOR, fl, fv);
     CHECK(rc == RSP_ERR_SHAPE && strlen(rsp_last_error(ctx)) > 0, "wrong P: status %d", rc);
